@@ -1,0 +1,323 @@
+"""TEST INFRASTRUCTURE ONLY (see oracle/__init__.py) — torch-CPU restatement of the reference.
+
+Every function cites the reference file:line it restates (paths under /root/reference).
+Two convention presets exist because the reference's three implementations disagree
+(SURVEY.md Appendix A.3):
+
+  preset "torch"  = path T, the default training path and the parity contract
+                    (gaussian_model/gaussian_model.py:253-364, nlos_helpers.py:124-232)
+  preset "cuda"   = path C, submodules/cuda_renderer/src/volume_renderer.cu:16-185 with
+                    include/cuda_utils.cuh:54-151 and include/spherical_harmonics.cuh:20-80,
+                    post-processing of gaussian_model/cuda_autograd.py:301-314
+
+Gradients are torch autograd through these restatements (the reference's own backward for
+path T is torch autograd too; path C's backward returns zeros, cuda_autograd.py:147-156).
+
+An optional Mahalanobis cutoff `mc` zeroes every sample whose whitened squared distance
+exceeds mc**2 — the exact support rule the HIP kernels implement; mc=None is the dense
+reference semantics.
+"""
+import math
+
+import torch
+
+C0 = 0.28209479177387814
+C1 = 0.4886025119029199
+C2 = [1.0925484305920792, -1.0925484305920792, 0.31539156525252005, -1.0925484305920792,
+      0.5462742152960396]
+C3 = [-0.5900435899266435, 2.890611442640554, -0.4570457994644658, 0.3731763325901154,
+      -0.4570457994644658, 1.445305721320277, -0.5900435899266435]
+
+
+# --------------------------------------------------------------------------------------------
+# geometry: nlos_helpers.py:87-188
+# --------------------------------------------------------------------------------------------
+def cartesian2spherical(pt):
+    """nlos_helpers.py:87-95 — (x,y,z) -> (r, theta=acos(z/r), phi=atan2(y,x))."""
+    out = torch.zeros(pt.shape, dtype=pt.dtype)
+    r = torch.linalg.norm(pt, dim=1)
+    out[:, 0] = r
+    out[:, 1] = torch.acos(pt[:, 2] / r)
+    out[:, 2] = torch.atan2(pt[:, 1], pt[:, 0])
+    return out
+
+
+def spherical2cartesian(pt):
+    """nlos_helpers.py:98-104."""
+    out = torch.zeros(pt.shape, dtype=pt.dtype)
+    out[:, 0] = pt[:, 0] * torch.sin(pt[:, 1]) * torch.cos(pt[:, 2])
+    out[:, 1] = pt[:, 0] * torch.sin(pt[:, 1]) * torch.sin(pt[:, 2])
+    out[:, 2] = pt[:, 0] * torch.cos(pt[:, 1])
+    return out
+
+
+def volume_box_point(volume_position, volume_size):
+    """nlos_helpers.py:107-118 — the 8 corners in the reference's order."""
+    xv, yv, zv = [float(v) for v in volume_position]
+    h = volume_size / 2
+    x = [xv - h] * 4 + [xv + h] * 4
+    y = [yv - h, yv - h, yv + h, yv + h] * 2
+    z = [zv - h, zv + h] * 4
+    return torch.tensor([x, y, z], dtype=torch.float64).t().float()
+
+
+def sample_tables(p, box, ns, start, end, c, deltaT):
+    """nlos_helpers.py:124-188 (spherical_sample_histogram) for ONE wall point p [3].
+
+    Returns a dict with theta[ns], phi[ns], r[nr], I1, I2, dtheta, dphi, angle range and
+    input_points [Nr*ns*ns, 5] in the reference's (k, i, j) flatten order."""
+    bp = box - p[None, :]
+    sph = cartesian2spherical(bp)
+    tmin = torch.min(sph[:, 1]).item()
+    tmax = torch.max(sph[:, 1]).item()
+    pmin = torch.min(sph[:, 2]).item()
+    pmax = torch.max(sph[:, 2]).item()
+    theta = torch.linspace(tmin, tmax, ns, dtype=torch.float)
+    phi = torch.linspace(pmin, pmax, ns, dtype=torch.float)
+    dtheta = (tmax - tmin) / ns
+    dphi = (pmax - pmin) / ns
+    r_min = start * c * deltaT
+    r_max = end * c * deltaT
+    nr = end - start
+    r = torch.linspace(r_min, r_max, nr, dtype=torch.float)
+    I1 = math.floor(r_min / (c * deltaT))
+    I2 = math.ceil(r_max / (c * deltaT))
+    grid = torch.stack(torch.meshgrid(r, theta, phi, indexing="ij"), dim=-1)
+    sph = grid.reshape(-1, 3)
+    cart = spherical2cartesian(sph) + p
+    ip = torch.cat((cart, sph[:, 1:3]), dim=1).float()
+    return dict(theta=theta, phi=phi, r=r, I1=I1, I2=I2, nr=nr, dtheta=dtheta, dphi=dphi,
+                theta_min=tmin, theta_max=tmax, phi_min=pmin, phi_max=pmax, input_points=ip)
+
+
+# --------------------------------------------------------------------------------------------
+# Gaussian math
+# --------------------------------------------------------------------------------------------
+def build_rotation(r):
+    """gaussian_utils.py:189-210 — normalises (no eps) then the row-major rotation."""
+    norm = torch.sqrt(r[:, 0] * r[:, 0] + r[:, 1] * r[:, 1] + r[:, 2] * r[:, 2] + r[:, 3] * r[:, 3])
+    q = r / norm[:, None]
+    w, x, y, z = q[:, 0], q[:, 1], q[:, 2], q[:, 3]
+    R = torch.stack([
+        1 - 2 * (y * y + z * z), 2 * (x * y - w * z), 2 * (x * z + w * y),
+        2 * (x * y + w * z), 1 - 2 * (x * x + z * z), 2 * (y * z - w * x),
+        2 * (x * z - w * y), 2 * (y * z + w * x), 1 - 2 * (x * x + y * y)], dim=1)
+    return R.reshape(-1, 3, 3)
+
+
+def quat_to_rotmat_cuda(q):
+    """cuda_utils.cuh:54-85 — identity when |q| < 1e-8, else normalise once."""
+    norm = torch.sqrt((q * q).sum(dim=1))
+    safe = torch.where(norm < 1e-8, torch.ones_like(norm), norm)
+    qn = q / safe[:, None]
+    R = build_rotation(qn)  # build_rotation re-normalises; |qn| == 1 up to rounding
+    eye = torch.eye(3, dtype=q.dtype).expand_as(R)
+    return torch.where((norm < 1e-8)[:, None, None], eye, R)
+
+
+def eval_sh(deg, sh, dirs):
+    """sh_utils.py:57-112 (3DGS sign convention), degrees 0..3."""
+    assert 0 <= deg <= 3
+    result = C0 * sh[..., 0]
+    if deg > 0:
+        x, y, z = dirs[..., 0:1], dirs[..., 1:2], dirs[..., 2:3]
+        result = result - C1 * y * sh[..., 1] + C1 * z * sh[..., 2] - C1 * x * sh[..., 3]
+        if deg > 1:
+            xx, yy, zz = x * x, y * y, z * z
+            xy, yz, xz = x * y, y * z, x * z
+            result = (result + C2[0] * xy * sh[..., 4] + C2[1] * yz * sh[..., 5]
+                      + C2[2] * (2.0 * zz - xx - yy) * sh[..., 6]
+                      + C2[3] * xz * sh[..., 7] + C2[4] * (xx - yy) * sh[..., 8])
+            if deg > 2:
+                result = (result + C3[0] * y * (3 * xx - yy) * sh[..., 9]
+                          + C3[1] * xy * z * sh[..., 10]
+                          + C3[2] * y * (4 * zz - xx - yy) * sh[..., 11]
+                          + C3[3] * z * (2 * zz - 3 * xx - 3 * yy) * sh[..., 12]
+                          + C3[4] * x * (4 * zz - xx - yy) * sh[..., 13]
+                          + C3[5] * z * (xx - yy) * sh[..., 14]
+                          + C3[6] * x * (xx - 3 * yy) * sh[..., 15])
+    return result
+
+
+def eval_sh_cuda(deg, sh, dirs):
+    """spherical_harmonics.cuh:20-80 — same basis WITHOUT the 3DGS sign flips, and the
+    (3z^2-1), (5z^2-1), (5z^2-3) polynomial forms.  sh: [..., K], dirs: [..., 3] -> [...]."""
+    x, y, z = dirs[..., 0], dirs[..., 1], dirs[..., 2]
+    basis = [torch.full_like(x, C0)]
+    if deg >= 1:
+        basis += [C1 * y, C1 * z, C1 * x]
+    if deg >= 2:
+        basis += [1.0925484305920792 * x * y, 1.0925484305920792 * y * z,
+                  0.31539156525252005 * (3.0 * z * z - 1.0), 1.0925484305920792 * x * z,
+                  0.5462742152960396 * (x * x - y * y)]
+    if deg >= 3:
+        basis += [0.5900435899266435 * y * (3.0 * x * x - y * y), 2.890611442640554 * x * y * z,
+                  0.4570457994644658 * y * (5.0 * z * z - 1.0),
+                  0.3731763325901154 * z * (5.0 * z * z - 3.0),
+                  0.4570457994644658 * x * (5.0 * z * z - 1.0),
+                  1.445305721320277 * z * (x * x - y * y),
+                  0.5900435899266435 * x * (x * x - 3.0 * y * y)]
+    out = torch.zeros_like(x)
+    for i, b in enumerate(basis):
+        out = out + sh[..., i] * b
+    return out
+
+
+class Params:
+    """Raw Gaussian parameters with the reference GaussianModel's names
+    (gaussian_model/gaussian_model.py:38-49, features layout :120-123, :195-218)."""
+
+    def __init__(self, mu, scaling, rotation, opacity, features_dc, features_rest, active_sh_degree,
+                 requires_grad=True):
+        t = lambda a: torch.as_tensor(a, dtype=torch.float32).clone().requires_grad_(requires_grad)
+        self._mu = t(mu)
+        self._scaling = t(scaling)
+        self._rotation = t(rotation)
+        self._opacity = t(opacity)
+        self._features_dc = t(features_dc)
+        self._features_rest = t(features_rest)
+        self.active_sh_degree = int(active_sh_degree)
+
+    @property
+    def features(self):
+        return torch.cat((self._features_dc, self._features_rest), dim=1)  # [Ng, K, 1]
+
+    def leaves(self):
+        return [self._mu, self._scaling, self._rotation, self._opacity, self._features_dc,
+                self._features_rest]
+
+
+def gaussian_pdf(x, P, preset="torch", mod=1.0, mc=None):
+    """pdf [Ng, Na].
+
+    torch: gaussian_model.py:253-294  s = exp(exp(_scaling)*mod), u = R(q̂)(x-μ), no eps.
+    cuda : cuda_utils.cuh:124-151     s = exp(_scaling)*mod,    u = Rᵀ(x-μ), /(s+1e-8)."""
+    if preset == "torch":
+        scales = torch.exp(torch.exp(P._scaling) * mod)
+        rots = build_rotation(torch.nn.functional.normalize(P._rotation))
+        diff = x.unsqueeze(0) - P._mu.unsqueeze(1)
+        T = torch.matmul(rots.unsqueeze(1), diff.unsqueeze(-1)).squeeze(-1)
+        m2 = torch.sum((T / scales.unsqueeze(1)) ** 2, dim=-1)
+    else:
+        scales = torch.exp(P._scaling) * mod + 1e-8
+        rots = quat_to_rotmat_cuda(P._rotation)
+        diff = x.unsqueeze(0) - P._mu.unsqueeze(1)
+        T = torch.matmul(rots.transpose(1, 2).unsqueeze(1), diff.unsqueeze(-1)).squeeze(-1)
+        m2 = torch.sum((T / scales.unsqueeze(1)) ** 2, dim=-1)
+    pdf = torch.exp(-0.5 * m2)
+    if mc is not None:
+        pdf = torch.where(m2 <= mc * mc, pdf, torch.zeros_like(pdf))
+    return pdf
+
+
+def albedo(P, p, preset="torch", deg=None):
+    """ρ_g(p) = max(0, 0.5 + SH(d̂)·f), d̂ = (μ-p)/|μ-p|.
+    torch: gaussian_model.py:350-355 (eval_sh, /norm, no eps); cuda: volume_renderer.cu:109-111."""
+    deg = P.active_sh_degree if deg is None else deg
+    d = P._mu - p.unsqueeze(0)
+    if preset == "torch":
+        dn = d / d.norm(dim=1, keepdim=True)
+        K = P.features.shape[1]
+        shs = P.features.transpose(1, 2).view(-1, 1, K)
+        sh = eval_sh(deg, shs, dn)  # [Ng, 1]
+    else:
+        dn = d * (1.0 / (torch.sqrt((d * d).sum(dim=1, keepdim=True)) + 1e-8))
+        f = P.features[:, :, 0]
+        sh = eval_sh_cuda(deg, f, dn).unsqueeze(1)
+    return torch.clamp_min(sh + 0.5, 0.0)  # [Ng, 1]
+
+
+# --------------------------------------------------------------------------------------------
+# one wall point: gaussian_transient_rendering (nlos_helpers.py:192-232)
+# --------------------------------------------------------------------------------------------
+def render_wallpoint(P, p, tab, Y, c, deltaT, preset="torch", mode="noocl", mod=1.0, mc=None):
+    """Returns (result [Nr, Ns*Ns], hist [Nr]).
+
+    torch preset, mode 'noocl' : gaussian_model.py:346-364 + nlos_helpers.py:206-232
+    torch preset, mode 'netf'  : gaussian_model.py:297-325 (per-Gaussian self-transmittance)
+    cuda preset,  mode 'noocl' : volume_renderer.cu:138-183 (×cΔT) + cuda_autograd.py:301-314
+                                 (/(t²+1e-8)·sinθ, Σ·dθdφ) + nlos_helpers.py:275-276 (×Y²)."""
+    ns = tab["theta"].shape[0]
+    nr = tab["r"].shape[0]
+    x = tab["input_points"][:, 0:3]
+    pdf = gaussian_pdf(x, P, preset, mod, mc)
+    sig = torch.sigmoid(P._opacity)
+    rho = albedo(P, p, preset)
+    if mode == "noocl":
+        rho_density = torch.sum(pdf * sig * rho, dim=0)
+        if preset == "cuda":
+            rho_density = rho_density * c * deltaT
+    elif mode == "netf":
+        density = (pdf * sig).view(-1, nr, ns * ns)
+        occl = torch.exp(-density * c * deltaT)
+        trans = torch.cumprod(torch.cat([torch.ones([occl.shape[0], 1, occl.shape[2]]), occl + 1e-7], 1),
+                              1)[:, :-1, :]
+        rho_density = torch.sum(density.view(-1, nr * ns * ns) * trans.view(-1, nr * ns * ns) * rho,
+                                dim=0) * c * deltaT
+    else:
+        raise ValueError(mode)
+    result = rho_density.reshape(nr, ns * ns)
+    theta_grid = tab["input_points"].view(-1, ns * ns, 5)[:, :, 3]
+    if preset == "torch":
+        dist = (torch.linspace(tab["I1"], tab["I2"], nr, dtype=torch.float) * deltaT * c).view(-1, 1)
+        result = result / (dist ** 2) * torch.sin(theta_grid)
+    else:
+        t = torch.linspace(tab["I1"] * c * deltaT, tab["I2"] * c * deltaT, nr).view(-1, 1)
+        result = result / (t ** 2 + 1e-8) * torch.sin(theta_grid)
+    result = result * (Y ** 2)
+    hist = torch.sum(result, dim=1) * tab["dtheta"] * tab["dphi"]
+    return result, hist
+
+
+def render_volume(P, walls, box, Y, ns, start, end, c, deltaT, **kw):
+    """Loop of render_wallpoint over wall points [P,3] -> hist [P, Nr] (the reference renders one
+    wall point per step, main.py:198-269; the volume is the stack of those histograms)."""
+    hs = []
+    for w in range(walls.shape[0]):
+        tab = sample_tables(walls[w], box, ns, start, end, c, deltaT)
+        _, h = render_wallpoint(P, walls[w], tab, Y, c, deltaT, **kw)
+        hs.append(h)
+    return torch.stack(hs)
+
+
+def mse_loss(hist, target):
+    """compute_loss: MSELoss(mean) vs target (already × gt_times), nlos_helpers.py:323-327."""
+    loss = torch.mean((hist - target) ** 2)
+    return loss, loss / torch.mean(target ** 2)
+
+
+# --------------------------------------------------------------------------------------------
+# path C "rays" API: _C.render_rays (volume_renderer.cu:16-185, 189-305), dense (no AABB filter)
+# --------------------------------------------------------------------------------------------
+def render_rays_cuda(ray_o, ray_d, t, P, sh_features, cam, deg, c, deltaT, mod, use_occlusion, mc=None):
+    """Per-(ray, sample) outputs [N_rays, N_samples] x3 with the cuda conventions.
+
+    No-occlusion branch volume_renderer.cu:138-183; occlusion branch :80-137 (shared T across
+    Gaussians, α = 1-exp(-σ pdf cΔT), early exit at T < 1e-4 zero-fills the rest)."""
+    nrays, nsamp = ray_o.shape[0], t.shape[0]
+    x = (ray_o[:, None, :] + ray_d[:, None, :] * t[None, :, None]).reshape(-1, 3)
+    pdf = gaussian_pdf(x, P, "cuda", mod, mc)                       # [Ng, R*S]
+    sig = torch.sigmoid(P._opacity)                                  # [Ng,1]
+    d = P._mu - cam.unsqueeze(0)
+    dn = d * (1.0 / (torch.sqrt((d * d).sum(dim=1, keepdim=True)) + 1e-8))
+    rho = torch.clamp_min(eval_sh_cuda(deg, sh_features, dn) + 0.5, 0.0).unsqueeze(1)
+    contrib = pdf * sig
+    density = contrib.sum(0).view(nrays, nsamp)
+    if not use_occlusion:
+        rho_density = (contrib * rho).sum(0).view(nrays, nsamp) * c * deltaT
+        return rho_density, density, torch.ones_like(density)
+    alpha = 1.0 - torch.exp(-contrib * c * deltaT)
+    wa = (alpha * rho).sum(0).view(nrays, nsamp)
+    rd = torch.zeros(nrays, nsamp)
+    de = torch.zeros(nrays, nsamp)
+    tr = torch.zeros(nrays, nsamp)
+    for ri in range(nrays):
+        T = torch.ones(())
+        for s in range(nsamp):
+            de[ri, s] = density[ri, s]
+            tr[ri, s] = T
+            rd[ri, s] = T * wa[ri, s]
+            T = T * torch.exp(-density[ri, s] * c * deltaT)
+            if T.item() < 1e-4:
+                break
+    return rd, de, tr
