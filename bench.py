@@ -1,0 +1,194 @@
+"""Benchmark: transient volumes/sec (fwd+bwd), 100k Gaussians -> 128x128x1024 ToF bins (BASELINE.json).
+
+One step = render the whole 128x128-wall-point x 1024-bin transient volume (32x32 angular
+samples per wall point, "cuda" preset, no occlusion), MSE against a target volume, backward to
+the gradients of all six raw Gaussian parameter tensors.  Inputs are resident in HBM before the
+timed region.  With N ranks (one process per GPU, RCCL): every rank renders one full volume of
+its own capture (same scene, distinct target), gradients are summed with one all-reduce per
+step -> weak scaling, value = N volumes per step / max-over-ranks step time.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config C3] [--cutoff 3.0]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "nlos-gaussian-renderer_amd"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+CONFIGS = {
+    # name: (Ng, H, W, T, Ns, fwd_only)
+    "C1": (1_000, 32, 32, 128, 32, False),
+    "C2": (50_000, 64, 64, 512, 32, True),
+    "C3": (100_000, 128, 128, 1024, 32, False),
+    "C5": (500_000, 256, 256, 2048, 32, False),
+    "S1": (20_000, 32, 32, 512, 32, False),      # quick iteration size (not a BASELINE config)
+}
+PEAK_HBM_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+PEAK_FP32_TFLOPS = 157.3       # FP32 vector peak (the path has no MFMA shape)
+
+
+def param_bytes(deg):
+    return 4 * (3 + 3 + 4 + 1 + (deg + 1) ** 2)        # 108 B at SH degree 3
+
+
+def cpu_baseline(cfg_name, seed=0):
+    """Time the CPU oracle (dense restatement of the reference, cuda preset) on a bounded sample of
+    the same workload: 1 wall point x G_SAMPLE of the Ng Gaussians x the full Ns^2 x T sample grid,
+    fwd+bwd; extrapolated linearly (cost is linear in Gaussians and in wall points)."""
+    from nlosgr.volume import Scene
+    from oracle import torch_ref as R
+    ng, H, W, T, ns, _ = CONFIGS[cfg_name]
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    scene = Scene(H=H, W=W, T=T, ns=ns)
+    g_sample = max(1, min(ng, int(os.environ.get("NLOSGR_CPU_SAMPLE_G", "16"))))
+    from nlosgr.model import GaussianParams
+    m = GaussianParams.synthetic(ng, 3, preset="cuda", device="cpu", seed=seed)
+    sl = slice(0, g_sample)
+    P = R.Params(m._mu.detach()[sl], m._scaling.detach()[sl], m._rotation.detach()[sl], m._opacity.detach()[sl],
+                 m._features_dc.detach()[sl], m._features_rest.detach()[sl], 3)
+    walls = scene.walls("cpu")
+    box = scene.box("cpu")
+    p = walls[(H // 2) * W + W // 2]
+    tab = R.sample_tables(p, box, ns, scene.start, scene.end, scene.c, scene.deltaT)
+    # warm-up on a small radial slice, then the timed full sample
+    t0 = time.perf_counter()
+    _, h = R.render_wallpoint(P, p, tab, 0.5, scene.c, scene.deltaT, preset="cuda", mode="noocl")
+    (h * h).sum().backward()
+    t = time.perf_counter() - t0
+    per_volume = t * (ng / g_sample) * (H * W)
+    return {"value": 1.0 / per_volume, "unit": "volumes/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/torch_ref dense (cuda preset) fwd+bwd of 1 wall point x {g_sample} of {ng} "
+                      f"Gaussians x {ns}x{ns}x{T} samples = {t:.2f} s on {threads} threads; "
+                      f"extrapolated x{ng // g_sample} Gaussians x{H * W} wall points"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="C3")
+    ap.add_argument("--cutoff", type=float, default=3.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--profile-json", default="")
+    a = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    dev = torch.device("cuda", local)
+
+    from nlosgr import GaussianParams
+    from nlosgr.model import features_flat
+    from nlosgr.render import render_backward, render_forward
+    from nlosgr.volume import Scene, make_config, volume_loss
+
+    ng, H, W, T, ns, fwd_only = CONFIGS[a.config]
+    scene = Scene(H=H, W=W, T=T, ns=ns)
+    model = GaussianParams.synthetic(ng, 3, preset="cuda", device=dev, seed=0)
+    geo = scene.geometry(dev, "cuda", "noocl")
+    cfg = make_config(model, scene, "cuda", "noocl", cutoff=a.cutoff)
+    g = torch.Generator().manual_seed(1 + rank)
+    target = (torch.rand(H * W, T, generator=g) * 1e-3 * 100).to(dev)   # gt_times=100 (configs/default.py:12)
+    feats = features_flat(model).detach().contiguous()
+    params = [model._mu.detach(), model._scaling.detach(), model._rotation.detach(), model._opacity.detach(), feats]
+    stream = torch.cuda.current_stream(dev)
+    ev_fwd = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    ev_bwd = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    fwd_ms, bwd_ms = [], []
+
+    def step(timed):
+        if timed:
+            ev_fwd[0].record(stream)
+        hist, _ = render_forward(*params, geo, cfg, True, False)
+        if timed:
+            ev_fwd[1].record(stream)
+        if fwd_only:
+            return hist
+        # MSE (nlos_helpers.py:325) over the volume; dL/dhist computed in closed form
+        grad = (2.0 / hist.numel()) * (hist - target)
+        if timed:
+            ev_bwd[0].record(stream)
+        grads = render_backward(*params, geo, cfg, grad_hist=grad)
+        if timed:
+            ev_bwd[1].record(stream)
+        if world > 1:
+            flat = torch.cat([t.reshape(-1) for t in grads])
+            dist.all_reduce(flat)
+        return grads
+
+    for _ in range(a.warmup):
+        step(False)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step(True)
+        torch.cuda.synchronize(dev)
+        fwd_ms.append(ev_fwd[0].elapsed_time(ev_fwd[1]))
+        if not fwd_only:
+            bwd_ms.append(ev_bwd[0].elapsed_time(ev_bwd[1]))
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    ms_per_step = elapsed * 1000.0 / a.steps
+    volumes_per_s = world * a.steps / elapsed
+
+    # roofline of the dominant kernel (algorithmic HBM bytes / measured launch time)
+    pb = param_bytes(3)
+    V = 4 * H * W * T
+    fwd_avg = sum(fwd_ms) / len(fwd_ms)
+    bwd_avg = sum(bwd_ms) / len(bwd_ms) if bwd_ms else 0.0
+    if bwd_avg >= fwd_avg:
+        dom, dom_ms, dom_bytes = "nlosgr bwd (preprocess+bwd_kernel+finish)", bwd_avg, 2 * ng * pb + V
+    else:
+        dom, dom_ms, dom_bytes = "nlosgr fwd (preprocess+fwd_kernel)", fwd_avg, ng * pb + V
+    achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
+    out = {
+        "metric": "transient volumes/sec (fwd+bwd), 100k Gaussians → 128×128×1024 ToF bins"
+        if a.config == "C3" else f"transient volumes/sec ({'fwd' if fwd_only else 'fwd+bwd'}) {a.config}",
+        "value": volumes_per_s, "unit": "volumes/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+        "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "f32", "data": "synthetic (SURVEY §8d geometry, seeded random Gaussians and target)",
+        "config": {"workload": f"{a.config}: {ng} Gaussians -> {H}x{W} wall x {T} bins, {ns}x{ns} angular "
+                               f"samples, cuda preset, no occlusion, support cutoff {a.cutoff} sigma, "
+                               f"{'fwd' if fwd_only else 'fwd+MSE+bwd (6 param grads)'}",
+                   "gaussians": ng, "wall": [H, W], "bins": T, "angular": ns, "cutoff": a.cutoff,
+                   "parallelism": f"wall-replica x{world}, grad all-reduce" if world > 1 else "single GPU"},
+        "phase_ms": {"fwd": fwd_avg, "bwd": bwd_avg},
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                     "frac": achieved / PEAK_HBM_GBS, "traffic": None,
+                     "algorithmic_bytes_per_launch": dom_bytes, "avg_launch_ms": dom_ms},
+    }
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        try:
+            out["cpu_baseline"] = cpu_baseline(a.config)
+        except Exception as e:  # report, never fake
+            out["cpu_baseline"] = {"value": None, "error": repr(e)}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,125 @@
+/*
+ * nlosgr.h — C ABI of the MI355X-native transient Gaussian NLOS renderer.
+ *
+ * Plain pointers and sizes only (no torch types).  Every device pointer is a gfx950 HBM
+ * address owned by the caller; the library never allocates device memory: callers size the
+ * scratch with nlosgr_workspace_bytes() and pass it in.  All work is enqueued on the given
+ * HIP stream; no call synchronises the device.  Return value 0 = success, otherwise a
+ * NLOSGR_E_* code with a message in nlosgr_last_error() (thread-local).
+ *
+ * Reference interfaces these entry points replace (paths under the reference repo):
+ *   nlosgr_render_fwd   <- _C.render_rays            submodules/cuda_renderer/include/volume_renderer.h:8-24,
+ *                                                    src/volume_renderer.cu:189-305
+ *                       <- GaussianModel.estimate_rho_w_no_occlusion / estimate_rho_w('netf')
+ *                          + gaussian_transient_rendering (the dense torch path that actually runs):
+ *                          gaussian_model/gaussian_model.py:297-364, nlos_helpers.py:192-232
+ *   nlosgr_render_bwd   <- CUDARenderFunction.backward gaussian_model/cuda_autograd.py:110-191
+ *                          (zeros in the reference; real gradients here) and torch autograd of path T
+ *   nlosgr_bboxes       <- compute_gaussian_bboxes_kernel include/bbox_compute.cuh:76-120,
+ *                          GaussianModel.get_bboxes gaussian_model/gaussian_model.py:140-178
+ */
+#ifndef NLOSGR_H
+#define NLOSGR_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NLOSGR_ABI_VERSION 1
+
+/* convention presets */
+enum {
+    NLOSGR_PRESET_TORCH = 0, /* path T: s=exp(exp(S)*mod), u=R(x-mu), 3DGS SH signs, no eps */
+    NLOSGR_PRESET_CUDA = 1   /* path C: s=exp(S)*mod, u=R^T(x-mu)/(s+1e-8), unsigned SH, eps'd normalise */
+};
+
+/* per-sample density model */
+enum {
+    NLOSGR_MODE_NOOCL = 0, /* rho_d = sum_g sigma pdf rho                  (gaussian_model.py:346-364) */
+    NLOSGR_MODE_NETF = 1   /* per-Gaussian self-transmittance cumprod       (gaussian_model.py:313-324) */
+};
+
+enum {
+    NLOSGR_OK = 0,
+    NLOSGR_E_INVALID = 1, /* bad argument / shape */
+    NLOSGR_E_HIP = 2,     /* HIP launch error */
+    NLOSGR_E_UNSUPPORTED = 3
+};
+
+/* Gaussians: raw (pre-activation) parameters, exactly the reference GaussianModel tensors. */
+typedef struct {
+    int32_t ng;               /* number of Gaussians */
+    int32_t k_feat;           /* feature row stride K >= (sh_degree+1)^2, K <= 16 */
+    int32_t sh_degree;        /* active SH degree, 0..3 */
+    int32_t preset;           /* NLOSGR_PRESET_* */
+    float scaling_modifier;   /* `mod` */
+    const float* mu;          /* [ng,3]  _mu                                         */
+    const float* scaling;     /* [ng,3]  _scaling (raw)                              */
+    const float* rotation;    /* [ng,4]  _rotation (raw quaternion w,x,y,z)          */
+    const float* opacity;     /* [ng]    _opacity (raw logit)                        */
+    const float* features;    /* [ng,k_feat] cat(_features_dc,_features_rest) flattened */
+} nlosgr_gaussians;
+
+/* Batched spherical sampling geometry: one (theta, phi, r) grid per relay-wall point, i.e. the
+ * reference's spherical_sample_histogram (nlos_helpers.py:124-188) for P wall points at once.
+ * Sample (p, k, i, j) sits at x = wall[p] + r[k] * (st_i cp_j, st_i sp_j, ct_i). */
+typedef struct {
+    int32_t nwall;            /* P */
+    int32_t nt;               /* theta samples (Ns in the reference) */
+    int32_t np;               /* phi samples (Ns in the reference) */
+    int32_t nr;               /* radial samples = time bins T */
+    const float* wall;        /* [P,3] wall points */
+    const float* sin_theta;   /* [P,nt] */
+    const float* cos_theta;   /* [P,nt] */
+    const float* sin_phi;     /* [P,np] */
+    const float* cos_phi;     /* [P,np] */
+    const float* grid_lin;    /* [P,4] (theta_min, theta_step, phi_min, phi_step) of the linspace grids */
+    const float* hscale;      /* [P] histogram weight per wall point (dtheta*dphi*Y^2[*c*dT]) */
+    const float* r;           /* [nr] sample radii (linspace, shared by all wall points) */
+    const float* att;         /* [nr] per-bin attenuation (1/dist^2 or 1/(t^2+1e-8)) */
+} nlosgr_geometry;
+
+typedef struct {
+    int32_t mode;             /* NLOSGR_MODE_* */
+    float cutoff;             /* Mahalanobis support radius m_c; <= 0 -> dense (no culling) */
+    float c_deltaT;           /* c * deltaT (netf transmittance) */
+    float ray_scale;          /* scale applied to the optional per-ray output (e.g. c*dT) */
+    int32_t nsplit;           /* backward: wall-point splits (0 -> auto) */
+    int32_t flags;            /* reserved, 0 */
+} nlosgr_options;
+
+/* Scratch bytes needed by fwd/bwd for this problem (caller allocates, 256-B aligned). */
+size_t nlosgr_workspace_bytes(const nlosgr_gaussians* g, const nlosgr_geometry* geo,
+                              const nlosgr_options* opt);
+
+/* Forward.  hist_out [P,nr] (may be NULL):  hscale[p]*att[k]*sum_{g,i,j} w_g(p) sin(theta_i) pdf
+ *           ray_out  [P,nt*np,nr] (may be NULL, caller zero-fills): ray_scale*sum_g w_g(p) pdf,
+ *           rays in the reference's (i,j) meshgrid('ij') order, samples contiguous — the layout of
+ *           _C.render_rays' rho_density [N_rays, N_samples].
+ * w_g(p) = sigmoid(opacity_g) * max(0, 0.5 + SH_g(dir(mu_g - wall_p))). */
+int nlosgr_render_fwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo,
+                      const nlosgr_options* opt, void* workspace, float* hist_out,
+                      float* ray_out, void* hip_stream);
+
+/* Backward.  grad_hist [P,nr] and/or grad_ray [P,nt*np,nr] (either may be NULL).
+ * Writes (overwrites) the gradients of the RAW parameters: d_mu [ng,3], d_scaling [ng,3],
+ * d_rotation [ng,4], d_opacity [ng], d_features [ng,k_feat]. */
+int nlosgr_render_bwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo,
+                      const nlosgr_options* opt, void* workspace, const float* grad_hist,
+                      const float* grad_ray, float* d_mu, float* d_scaling, float* d_rotation,
+                      float* d_opacity, float* d_features, void* hip_stream);
+
+/* 3-sigma (sigma_scale) axis-aligned boxes [ng,6] = (min xyz, max xyz) under the preset's scale
+ * convention (bbox_compute.cuh:23-71 for "cuda"; gaussian_model.py:140-178 for "torch"). */
+int nlosgr_bboxes(const nlosgr_gaussians* g, float sigma_scale, float* bboxes_out, void* hip_stream);
+
+const char* nlosgr_last_error(void);
+int nlosgr_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NLOSGR_H */

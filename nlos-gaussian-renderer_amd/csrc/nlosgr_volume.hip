@@ -1,0 +1,981 @@
+// Transient Gaussian NLOS renderer — volume forward / backward kernels and the C ABI (gfx950).
+//
+// Hot path: for every relay-wall point p and time bin k
+//     hist[p,k] = hscale[p] * att[k] * sum_g w_g(p) sum_{i,j} sin(theta_i) pdf_g(p + r_k d_ij)
+// (no-occlusion) or the per-Gaussian self-transmittance variant ('netf').
+//
+// Algebra that makes the inner loop cheap: with u0 = A(p - mu) and v = A d_ij the whitened
+// offset along ray ij is u(r) = u0 + r v, a straight line, so each (pair, ray) is a 1-D
+// Gaussian in r:  pdf(r) = exp(-(m2min + a (r - t*)^2) / 2),  a = |v|^2, t* = -(u0.v)/a,
+// m2min = |u0 + t* v|^2.  The support |u| <= m_c is
+//   * per pair: a cone of rays (bounding-sphere test -> (theta, phi) index box), then
+//   * per ray:  the quadric d^T M d >= 0,  M = (A^T u0)(A^T u0)^T - (|u0|^2 - m_c^2) A^T A
+//               (exactly m2min <= m_c^2), then
+//   * per ray:  one contiguous bin range [kl, kh] (a "segment").
+//
+// Work decomposition (4 independent waves per workgroup; no global atomics on the hot path):
+//   forward : workgroup = one wall point.  Lane = (wall point, Gaussian) pair enumerates its
+//             candidate rays; passing rays become segments in a wave-private LDS queue.  The
+//             queue is drained 64 bins at a time with lane = bin: conflict-free adds into a
+//             wave-private LDS histogram, flushed periodically (round-to-nearest) into a
+//             wave-private total (LDS float atomics accumulate with a downward bias when a bin
+//             collects thousands of adds).  The 4 totals are summed in a fixed order, so the
+//             forward is bitwise deterministic.
+//   backward: workgroup = 64 Gaussians x a split of the wall; wave w walks wall points
+//             w, w+4, ...  Lane = segment runs the bins of one ray serially with its sums in
+//             registers; per-pair sums in LDS; per-Gaussian accumulators stay in registers
+//             for the whole split and are combined in a fixed order into a partial slab.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "nlosgr_device.hpp"
+
+using namespace nlosgr;
+
+namespace {
+
+thread_local char g_err[512] = "";
+
+int set_err(int code, const char* msg) {
+    snprintf(g_err, sizeof(g_err), "%s", msg);
+    return code;
+}
+
+constexpr int kBlock = 256;
+constexpr int kWaves = kBlock / 64;
+constexpr int kMaxK = 16;
+constexpr int kQ = 128;          // segment queue capacity per wave (drained at >= 64)
+constexpr int kNB = 64;          // Gaussians per backward workgroup
+constexpr int kFlushRounds = 8;  // forward: Gaussian rounds between round-to-nearest flushes
+constexpr float kPi = 3.14159265358979323846f;
+constexpr float kHalfLog2e = 0.72134752044448170368f;  // log2(e)/2
+
+// float -> int index, saturated before the conversion (no UB for huge / non-finite values)
+__device__ __forceinline__ int fidx(float x, int lo, int hi) {
+    x = fminf(fmaxf(x, (float)lo), (float)hi);
+    return (int)x;
+}
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+
+__device__ __forceinline__ int lanes_below(unsigned long long mask) {
+    return __builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0));
+}
+
+// orders LDS traffic between lanes of one wave (no workgroup barrier needed)
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+}
+
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+struct KArgs {
+    nlosgr_gaussians g;
+    nlosgr_geometry geo;
+    nlosgr_options opt;
+    const GaussRec* recs;
+    float* hist_out;
+    float* ray_out;
+    const float* grad_hist;
+    const float* grad_ray;
+    float* partial;  // [nsplit][ng][32]
+    int nsplit;
+};
+
+// ------------------------------------------------------------------------------------------
+// preprocess: raw params -> A = diag(1/s~) R', sigma, s_max, N = A^T A
+// ------------------------------------------------------------------------------------------
+template <int PRESET>
+__global__ __launch_bounds__(kBlock) void preprocess_kernel(nlosgr_gaussians g, GaussRec* recs) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= g.ng) return;
+    float S[3] = {g.scaling[3 * i], g.scaling[3 * i + 1], g.scaling[3 * i + 2]};
+    float Q[4] = {g.rotation[4 * i], g.rotation[4 * i + 1], g.rotation[4 * i + 2], g.rotation[4 * i + 3]};
+    GaussAct a;
+    activate<PRESET>(S, Q, g.opacity[i], g.scaling_modifier, a);
+    float A[9];
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) A[3 * r + c] = a.Rp[3 * r + c] / a.st[r];
+    float N[6];
+    const int ix[6][2] = {{0, 0}, {0, 1}, {0, 2}, {1, 1}, {1, 2}, {2, 2}};
+    for (int t = 0; t < 6; ++t) {
+        const int p = ix[t][0], q = ix[t][1];
+        N[t] = A[p] * A[q] + A[3 + p] * A[3 + q] + A[6 + p] * A[6 + q];
+    }
+    const float smax = fmaxf(a.st[0], fmaxf(a.st[1], a.st[2]));
+    GaussRec rec;
+    rec.a = make_float4(g.mu[3 * i], g.mu[3 * i + 1], g.mu[3 * i + 2], a.sigma);
+    rec.b = make_float4(A[0], A[1], A[2], A[3]);
+    rec.c = make_float4(A[4], A[5], A[6], A[7]);
+    rec.d = make_float4(A[8], smax, N[0], N[1]);
+    rec.e = make_float4(N[2], N[3], N[4], N[5]);
+    recs[i] = rec;
+}
+
+// ------------------------------------------------------------------------------------------
+// per-(wall point, Gaussian) pair state
+// ------------------------------------------------------------------------------------------
+struct Pair {
+    float A[9], sigma, smax, N[6];
+    float q[3];         // p - mu
+    float u0[3];        // A (p - mu)
+    float dir[3], nrm;  // view direction of mu - p (preset convention)
+    float sh, rho, w;
+    float M[6];         // quadric (M00, 2M01, 2M02, M11, 2M12, M22)
+    int i0, i1, j0, j1;
+};
+
+__device__ __forceinline__ void load_rec(const GaussRec& r, Pair& P, float mu[3]) {
+    mu[0] = r.a.x; mu[1] = r.a.y; mu[2] = r.a.z; P.sigma = r.a.w;
+    P.A[0] = r.b.x; P.A[1] = r.b.y; P.A[2] = r.b.z; P.A[3] = r.b.w;
+    P.A[4] = r.c.x; P.A[5] = r.c.y; P.A[6] = r.c.z; P.A[7] = r.c.w;
+    P.A[8] = r.d.x; P.smax = r.d.y; P.N[0] = r.d.z; P.N[1] = r.d.w;
+    P.N[2] = r.e.x; P.N[3] = r.e.y; P.N[4] = r.e.z; P.N[5] = r.e.w;
+}
+
+template <int PRESET, bool DENSE>
+__device__ __forceinline__ void pair_setup(const KArgs& k, int gi, const float mu[3], float px, float py, float pz,
+                                           const float* lin, float mc2, Pair& P) {
+    P.q[0] = px - mu[0]; P.q[1] = py - mu[1]; P.q[2] = pz - mu[2];
+    for (int r = 0; r < 3; ++r) P.u0[r] = P.A[3 * r] * P.q[0] + P.A[3 * r + 1] * P.q[1] + P.A[3 * r + 2] * P.q[2];
+    view_dir<PRESET>(-P.q[0], -P.q[1], -P.q[2], P.dir[0], P.dir[1], P.dir[2], P.nrm);
+    const int deg = k.g.sh_degree;
+    const int K = (deg + 1) * (deg + 1);
+    float Y[kMaxK];
+    sh_basis<PRESET>(deg, P.dir[0], P.dir[1], P.dir[2], Y);
+    const float* f = k.g.features + (size_t)gi * k.g.k_feat;
+    float sh = 0.f;
+#pragma unroll
+    for (int c = 0; c < kMaxK; ++c)
+        if (c < K) sh += f[c] * Y[c];
+    P.sh = sh;
+    P.rho = fmaxf(sh + 0.5f, 0.0f);
+    P.w = P.sigma * P.rho;
+    const int nt = k.geo.nt, np_ = k.geo.np;
+    P.i0 = 0; P.i1 = nt - 1; P.j0 = 0; P.j1 = np_ - 1;
+    if (DENSE) return;
+    // quadric cone: d^T M d >= 0  <=>  m2min(d) <= m_c^2
+    const float wv0 = P.A[0] * P.u0[0] + P.A[3] * P.u0[1] + P.A[6] * P.u0[2];
+    const float wv1 = P.A[1] * P.u0[0] + P.A[4] * P.u0[1] + P.A[7] * P.u0[2];
+    const float wv2 = P.A[2] * P.u0[0] + P.A[5] * P.u0[1] + P.A[8] * P.u0[2];
+    const float kap = P.u0[0] * P.u0[0] + P.u0[1] * P.u0[1] + P.u0[2] * P.u0[2] - mc2;
+    P.M[0] = wv0 * wv0 - kap * P.N[0];
+    P.M[1] = 2.0f * (wv0 * wv1 - kap * P.N[1]);
+    P.M[2] = 2.0f * (wv0 * wv2 - kap * P.N[2]);
+    P.M[3] = wv1 * wv1 - kap * P.N[3];
+    P.M[4] = 2.0f * (wv1 * wv2 - kap * P.N[4]);
+    P.M[5] = wv2 * wv2 - kap * P.N[5];
+    // bounding-sphere cone -> (theta, phi) index box
+    const float Rb = k.opt.cutoff * P.smax * 1.0001f + 1e-7f;
+    const float dist = sqrtf(P.q[0] * P.q[0] + P.q[1] * P.q[1] + P.q[2] * P.q[2]);
+    if (dist <= Rb) return;
+    const float sa = Rb / dist;
+    const float alpha = asinf(fminf(sa, 1.0f));
+    const float cz = fminf(fmaxf(-P.q[2] / dist, -1.0f), 1.0f);
+    const float thc = acosf(cz);
+    const float th0 = lin[0], dth = lin[1], ph0 = lin[2], dph = lin[3];
+    if (dth > 0.f) {
+        P.i0 = fidx(floorf((thc - alpha - th0) / dth), 0, nt - 1);
+        P.i1 = fidx(ceilf((thc + alpha - th0) / dth), -1, nt - 1);
+    }
+    if (thc - alpha > 1e-6f && thc + alpha < kPi - 1e-6f && dph > 0.f) {
+        const float phc = atan2f(-P.q[1], -P.q[0]);
+        const float dphi = asinf(fminf(sa / sinf(thc), 1.0f));
+        const float lo = phc - dphi, hi = phc + dphi;
+        if (lo > -kPi && hi < kPi) {
+            P.j0 = fidx(floorf((lo - ph0) / dph), 0, np_ - 1);
+            P.j1 = fidx(ceilf((hi - ph0) / dph), -1, np_ - 1);
+        }
+    }
+}
+
+__device__ __forceinline__ float quadric(const float* M, float dx, float dy, float dz) {
+    const float t0 = fmaf(M[0], dx, fmaf(M[1], dy, M[2] * dz));
+    const float t1 = fmaf(M[3], dy, M[4] * dz);
+    return fmaf(dx, t0, fmaf(dy, t1, dz * dz * M[5]));
+}
+
+// Ray quantities: v = A d, a = |v|^2, t*, z* = u0 + t* v, m2min, in-support bin range.
+struct Ray {
+    float v[3], a, ts, zs[3], m2min;
+    int kl, kh;
+};
+
+template <bool DENSE>
+__device__ __forceinline__ bool ray_setup(const float* A, const float* u0, float dx, float dy, float dz, float mc2,
+                                          float r0, float dr, int nr, Ray& R) {
+    for (int r = 0; r < 3; ++r) R.v[r] = A[3 * r] * dx + A[3 * r + 1] * dy + A[3 * r + 2] * dz;
+    R.a = R.v[0] * R.v[0] + R.v[1] * R.v[1] + R.v[2] * R.v[2];
+    const float b = u0[0] * R.v[0] + u0[1] * R.v[1] + u0[2] * R.v[2];
+    R.ts = -b / R.a;
+    for (int r = 0; r < 3; ++r) R.zs[r] = u0[r] + R.ts * R.v[r];
+    R.m2min = R.zs[0] * R.zs[0] + R.zs[1] * R.zs[1] + R.zs[2] * R.zs[2];
+    if (DENSE) {
+        R.kl = 0; R.kh = nr - 1;
+        return true;
+    }
+    if (!(R.m2min <= mc2)) return false;
+    const float h = sqrtf((mc2 - R.m2min) / R.a);
+    if (dr > 0.f) {
+        R.kl = fidx(ceilf((R.ts - h - r0) / dr), 0, nr);
+        R.kh = fidx(floorf((R.ts + h - r0) / dr), -1, nr - 1);
+    } else {
+        R.kl = 0; R.kh = nr - 1;
+    }
+    return R.kl <= R.kh;
+}
+
+// LDS carve helper (offsets in floats, 16-byte aligned)
+__host__ __device__ __forceinline__ int al4(int n) { return (n + 3) & ~3; }
+
+struct FwdLayout {
+    int acc, tot, queue, qx, qray, wave_stride, total;
+    __host__ __device__ FwdLayout(int nr, int nt, int np_) {
+        const int off = al4(2 * (nt + np_));  // float2 theta table [nt], float2 phi table [np]
+        acc = 0;                              // [nr + 64] window target (+64: windows overrun nr)
+        tot = al4(nr + 64);                   // [nr] round-to-nearest totals
+        queue = tot + al4(nr);                // float4 [kQ] (alpha, gamma, lam_s, kl|len)
+        qx = queue + 4 * kQ;                  // float4 [kQ] (sin theta, sigma c dT, w c dT, ray)
+        qray = qx + 4 * kQ;
+        wave_stride = al4(qray);
+        acc += off; tot += off; queue += off; qx += off;
+        total = off + kWaves * wave_stride;
+    }
+};
+
+// ------------------------------------------------------------------------------------------
+// forward
+// ------------------------------------------------------------------------------------------
+template <int MODE, bool RAYS>
+__device__ __forceinline__ void fwd_drain(float* acc, const float4* queue, const float4* qx, int cnt, float* rout,
+                                          int nr, float rscale, float f0log2) {
+    const int lane = lane_id();
+    for (int s = 0; s < cnt; ++s) {
+        const float4 rec = queue[s];
+        const float4 ex = qx[s];
+        const unsigned bits = __float_as_uint(rec.w);
+        const int kl = bits & 0xFFFF, len = bits >> 16;
+        float* dst = acc + kl;
+        float* rrow = RAYS ? rout + (size_t)__float_as_int(ex.w) * nr + kl : nullptr;
+        if (MODE == NLOSGR_MODE_NOOCL) {
+            // value = w pdf = exp2(alpha + gamma (lam - lam_s)^2); histogram adds sin(theta) x value
+            for (int m0 = 0; m0 < len; m0 += 64) {
+                const int lam = m0 + lane;
+                if (lam < len) {
+                    const float t = (float)lam - rec.z;
+                    const float val = fast_exp2(fmaf(rec.y, t * t, rec.x));
+                    atomicAdd(dst + lam, ex.x * val);
+                    if (RAYS) atomicAdd(rrow + lam, rscale * val);
+                }
+            }
+        } else {
+            // netf: T_k = prod_{k'<k} (exp(-sigma pdf c dT) + 1e-7) front-to-back along the ray
+            // (gaussian_model.py:317-321), an exclusive log-domain prefix scan across the window's
+            // lanes with the carry kept between windows; value = w c dT pdf T.
+            float logT = (float)kl * f0log2;
+            for (int m0 = 0; m0 < len; m0 += 64) {
+                const int lam = m0 + lane;
+                const bool in = lam < len;
+                const float t = (float)lam - rec.z;
+                const float pdf = in ? fast_exp2(fmaf(rec.y, t * t, rec.x)) : 0.f;
+                const float lf = in ? __log2f(__expf(-ex.y * pdf) + 1e-7f) : 0.f;
+                float incl = lf;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const float u = __shfl_up(incl, o);
+                    if (lane >= o) incl += u;
+                }
+                if (in) {
+                    const float val = ex.z * pdf * fast_exp2(logT + (incl - lf));
+                    atomicAdd(dst + lam, ex.x * val);
+                    if (RAYS) atomicAdd(rrow + lam, rscale * val);
+                }
+                logT += __shfl(incl, 63);
+            }
+        }
+    }
+}
+
+template <int PRESET, int MODE, bool DENSE, bool RAYS>
+__global__ __launch_bounds__(kBlock) void fwd_kernel(KArgs k) {
+    extern __shared__ __align__(16) float smem[];
+    const int nr = k.geo.nr, nt = k.geo.nt, np_ = k.geo.np;
+    const FwdLayout L(nr, nt, np_);
+    float2* tth = reinterpret_cast<float2*>(smem);
+    float2* tph = tth + nt;
+    const int wave = threadIdx.x >> 6, lane = lane_id();
+    float* wb = smem + wave * L.wave_stride;
+    float* acc = wb + L.acc;
+    float* tot = wb + L.tot;
+    float4* queue = reinterpret_cast<float4*>(wb + L.queue);
+    float4* qx = reinterpret_cast<float4*>(wb + L.qx);
+    const int p = blockIdx.x;
+
+    for (int t = threadIdx.x; t < nt; t += blockDim.x)
+        tth[t] = make_float2(k.geo.sin_theta[(size_t)p * nt + t], k.geo.cos_theta[(size_t)p * nt + t]);
+    for (int t = threadIdx.x; t < np_; t += blockDim.x)
+        tph[t] = make_float2(k.geo.cos_phi[(size_t)p * np_ + t], k.geo.sin_phi[(size_t)p * np_ + t]);
+    for (int t = lane; t < nr + 64; t += 64) acc[t] = 0.f;
+    for (int t = lane; t < nr; t += 64) tot[t] = 0.f;
+    __syncthreads();
+
+    const float px = k.geo.wall[3 * p], py = k.geo.wall[3 * p + 1], pz = k.geo.wall[3 * p + 2];
+    const float* lin = k.geo.grid_lin + 4 * (size_t)p;
+    const float mc2 = k.opt.cutoff * k.opt.cutoff;
+    const float r0 = k.geo.r[0];
+    const float dr = nr > 1 ? (k.geo.r[nr - 1] - r0) / (float)(nr - 1) : 0.f;
+    const float inv_dr = dr > 0.f ? 1.0f / dr : 0.f;
+    const float cdt = k.opt.c_deltaT;
+    const float f0log2 = log2f(1.0f + 1e-7f);
+    float* rout = RAYS ? k.ray_out + (size_t)p * nt * np_ * nr : nullptr;
+    const float rscale = k.opt.ray_scale;
+
+    int cnt = 0;
+    int round = 0;
+    for (int base = wave * 64; base < k.g.ng; base += kBlock, ++round) {
+        const int gi = base + lane;
+        Pair P;
+        float mu[3];
+        bool more = false;
+        P.i0 = P.i1 = P.j0 = P.j1 = 0;
+        if (gi < k.g.ng) {
+            load_rec(k.recs[gi], P, mu);
+            pair_setup<PRESET, DENSE>(k, gi, mu, px, py, pz, lin, mc2, P);
+            more = (P.w > 0.f) && P.i0 <= P.i1 && P.j0 <= P.j1;
+        }
+        int ci = P.i0, cj = P.j0;
+        const float lw = (MODE == NLOSGR_MODE_NOOCL && more) ? __log2f(P.w) : 0.f;
+        while (__builtin_amdgcn_ballot_w64(more)) {
+            bool pass = false;
+            float4 rec, ex;
+            if (more) {
+                const float2 th = tth[ci], ph = tph[cj];
+                const float dx = th.x * ph.x, dy = th.x * ph.y, dz = th.y;
+                if (DENSE || quadric(P.M, dx, dy, dz) >= 0.f) {
+                    Ray R;
+                    if (ray_setup<DENSE>(P.A, P.u0, dx, dy, dz, mc2, r0, dr, nr, R)) {
+                        // window coordinates lam = k - kl; log2(value) = alpha + gamma (lam - lam_s)^2
+                        rec = make_float4(lw - kHalfLog2e * R.m2min, -kHalfLog2e * R.a * dr * dr,
+                                          (R.ts - r0) * inv_dr - (float)R.kl,
+                                          __uint_as_float((unsigned)R.kl | ((unsigned)(R.kh - R.kl + 1) << 16)));
+                        ex = make_float4(th.x, P.sigma * cdt, P.w * cdt, __int_as_float(ci * np_ + cj));
+                        pass = true;
+                    }
+                }
+                if (++cj > P.j1) { cj = P.j0; ++ci; }
+                more = ci <= P.i1;
+            }
+            const unsigned long long m = __builtin_amdgcn_ballot_w64(pass);
+            if (pass) {
+                const int pos = cnt + lanes_below(m);
+                queue[pos] = rec;
+                qx[pos] = ex;
+            }
+            cnt += __popcll(m);
+            if (cnt >= 64) {
+                wave_sync();
+                fwd_drain<MODE, RAYS>(acc, queue, qx, cnt, rout, nr, rscale, f0log2);
+                wave_sync();
+                cnt = 0;
+            }
+        }
+        if ((round + 1) % kFlushRounds == 0) {
+            wave_sync();
+            fwd_drain<MODE, RAYS>(acc, queue, qx, cnt, rout, nr, rscale, f0log2);
+            cnt = 0;
+            wave_sync();
+            for (int t = lane; t < nr; t += 64) {
+                tot[t] += acc[t];
+                acc[t] = 0.f;
+            }
+            wave_sync();
+        }
+    }
+    wave_sync();
+    fwd_drain<MODE, RAYS>(acc, queue, qx, cnt, rout, nr, rscale, f0log2);
+    wave_sync();
+    for (int t = lane; t < nr; t += 64) tot[t] += acc[t];
+    __syncthreads();
+    if (k.hist_out) {
+        const float hs = k.geo.hscale[p];
+        for (int t = threadIdx.x; t < nr; t += blockDim.x) {
+            float s = 0.f;
+            for (int w = 0; w < kWaves; ++w) s += smem[w * L.wave_stride + L.tot + t];
+            k.hist_out[(size_t)p * nr + t] = s * k.geo.att[t] * hs;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// backward
+// ------------------------------------------------------------------------------------------
+struct BwdLayout {
+    int recs, wave_base, wave_stride, grow, tth, tph, pd, prho, pacc, queue, red, total;
+    __host__ __device__ BwdLayout(int nr, int nt, int np_) {
+        recs = 0;                            // GaussRec [kNB] (20 floats each)
+        wave_base = al4(kNB * 20);
+        grow = 0;                            // [nr] upstream gradient row x att x hscale
+        tth = al4(nr);                       // float2 [nt]
+        tph = tth + al4(2 * nt);             // float2 [np]
+        pd = tph + al4(2 * np_);             // float4 [64] (u0, w)
+        prho = pd + 4 * 64;                  // [64] rho
+        pacc = prho + 64;                    // [64][16] per-pair accumulators
+        queue = pacc + 16 * 64;              // uint2 [kQ]
+        wave_stride = al4(queue + 2 * kQ);
+        red = wave_base;                     // final reduction reuses the wave regions
+        total = wave_base + kWaves * wave_stride;
+        const int need_red = wave_base + kWaves * 64 * 29;
+        if (need_red > total) total = need_red;
+    }
+};
+
+template <int MODE, bool RAYS>
+__device__ __forceinline__ void bwd_drain(const GaussRec* srec, const float* grow, const float2* tth,
+                                          const float2* tph, const float4* pd, const float* prho, float* pacc,
+                                          const uint2* queue, int cnt, const float* gray, int np_, float r0, float dr,
+                                          int nr, float cdt, float f0log2, float rscale) {
+    const int lane = lane_id();
+    if (lane >= cnt) return;
+    const uint2 e = queue[lane];
+    const int slot = e.x & 0xFF, i = (e.x >> 8) & 0xFFF, j = e.x >> 20;
+    const int kl = e.y & 0xFFFF, kh = e.y >> 16;
+    const float4 pdat = pd[slot];
+    const float u0[3] = {pdat.x, pdat.y, pdat.z};
+    const float w = pdat.w;
+    const GaussRec rr = srec[slot];
+    const float A[9] = {rr.b.x, rr.b.y, rr.b.z, rr.b.w, rr.c.x, rr.c.y, rr.c.z, rr.c.w, rr.d.x};
+    const float sigma = rr.a.w;
+    const float rho = prho[slot];
+    const float2 th = tth[i], ph = tph[j];
+    const float dx = th.x * ph.x, dy = th.x * ph.y, dz = th.y;
+    Ray R;
+    ray_setup<true>(A, u0, dx, dy, dz, 0.f, r0, dr, nr, R);
+    const float sti = th.x;
+    const float* grw = RAYS && gray ? gray + (size_t)(i * np_ + j) * nr : nullptr;
+    float S0 = 0.f, S1 = 0.f, S2 = 0.f, dsig = 0.f, drho = 0.f;  // S_n = sum_k (dL/dpdf_k) pdf_k dl^n
+    if (MODE == NLOSGR_MODE_NOOCL) {
+        float Hs = 0.f;
+        for (int kk = kl; kk <= kh; ++kk) {
+            const float dl = fmaf((float)kk, dr, r0) - R.ts;
+            const float pdf = fast_exp2(-kHalfLog2e * fmaf(R.a * dl, dl, R.m2min));
+            float H = grow[kk] * sti;
+            if (RAYS && grw) H += grw[kk] * rscale;
+            const float hp = H * pdf;
+            Hs += hp;
+            const float t1 = hp * dl;
+            S0 += hp; S1 += t1; S2 = fmaf(t1, dl, S2);
+        }
+        dsig = Hs * rho;
+        drho = Hs * sigma;
+        S0 *= w; S1 *= w; S2 *= w;
+    } else {
+        // netf: dL/dD_j = c rho H_j T_j + (sum_{k>j} H_k out_k) f'_j / f_j, two forward passes
+        const float T0 = fast_exp2((float)kl * f0log2);
+        float T = T0, Etot = 0.f;
+        for (int kk = kl; kk <= kh; ++kk) {
+            const float dl = fmaf((float)kk, dr, r0) - R.ts;
+            const float pdf = fast_exp2(-kHalfLog2e * fmaf(R.a * dl, dl, R.m2min));
+            const float D = sigma * pdf;
+            float H = grow[kk] * sti;
+            if (RAYS && grw) H += grw[kk] * rscale;
+            Etot += H * cdt * rho * D * T;
+            T *= (__expf(-D * cdt) + 1e-7f);
+        }
+        T = T0;
+        float pre = 0.f;
+        for (int kk = kl; kk <= kh; ++kk) {
+            const float dl = fmaf((float)kk, dr, r0) - R.ts;
+            const float pdf = fast_exp2(-kHalfLog2e * fmaf(R.a * dl, dl, R.m2min));
+            const float D = sigma * pdf;
+            float H = grow[kk] * sti;
+            if (RAYS && grw) H += grw[kk] * rscale;
+            const float ee = __expf(-D * cdt);
+            const float f = ee + 1e-7f;
+            pre += H * cdt * rho * D * T;
+            const float dD = cdt * rho * H * T + (Etot - pre) * (-cdt * ee) / f;
+            drho += H * cdt * D * T;
+            dsig += dD * pdf;
+            const float hp = dD * sigma * pdf;
+            const float t1 = hp * dl;
+            S0 += hp; S1 += t1; S2 = fmaf(t1, dl, S2);
+            T *= f;
+        }
+    }
+    // pdf = exp(-|z|^2/2), z = z* + dl v  ->  dL/du0 = -sum P z,  dL/dv = -sum P r z
+    float* pa = pacc + slot * 16;
+    float zv[3], dV[3];
+    for (int r = 0; r < 3; ++r) {
+        zv[r] = S0 * R.zs[r] + S1 * R.v[r];
+        dV[r] = -(R.ts * zv[r] + S1 * R.zs[r] + S2 * R.v[r]);
+        atomicAdd(pa + r, -zv[r]);
+    }
+    for (int r = 0; r < 3; ++r) {  // dA += dV (x) d
+        atomicAdd(pa + 3 + 3 * r, dV[r] * dx);
+        atomicAdd(pa + 4 + 3 * r, dV[r] * dy);
+        atomicAdd(pa + 5 + 3 * r, dV[r] * dz);
+    }
+    atomicAdd(pa + 12, dsig);
+    atomicAdd(pa + 13, drho);
+}
+
+template <int PRESET, int MODE, bool DENSE, bool RAYS>
+__global__ __launch_bounds__(kBlock) void bwd_kernel(KArgs k) {
+    extern __shared__ __align__(16) float smem[];
+    const int nr = k.geo.nr, nt = k.geo.nt, np_ = k.geo.np, P_ = k.geo.nwall;
+    const BwdLayout L(nr, nt, np_);
+    GaussRec* srec = reinterpret_cast<GaussRec*>(smem + L.recs);
+    const int wave = threadIdx.x >> 6, lane = lane_id();
+    float* wb = smem + L.wave_base + wave * L.wave_stride;
+    float* grow = wb + L.grow;
+    float2* tth = reinterpret_cast<float2*>(wb + L.tth);
+    float2* tph = reinterpret_cast<float2*>(wb + L.tph);
+    float4* pd = reinterpret_cast<float4*>(wb + L.pd);
+    float* prho = wb + L.prho;
+    float* pacc = wb + L.pacc;
+    uint2* queue = reinterpret_cast<uint2*>(wb + L.queue);
+
+    const int gb = blockIdx.x * kNB;
+    const int gi = gb + lane;
+    const bool active = gi < k.g.ng;
+    for (int t = threadIdx.x; t < kNB; t += blockDim.x)
+        if (gb + t < k.g.ng) srec[t] = k.recs[gb + t];
+    for (int t = lane; t < 64 * 16; t += 64) pacc[t] = 0.f;
+    __syncthreads();
+
+    const int split = blockIdx.y;
+    const int per = (P_ + k.nsplit - 1) / k.nsplit;
+    const int pbeg = split * per, pend = min(P_, pbeg + per);
+    const int deg = k.g.sh_degree;
+    const int K = (deg + 1) * (deg + 1);
+    const float mc2 = k.opt.cutoff * k.opt.cutoff;
+    const float r0 = k.geo.r[0];
+    const float dr = nr > 1 ? (k.geo.r[nr - 1] - r0) / (float)(nr - 1) : 0.f;
+    const float cdt = k.opt.c_deltaT;
+    const float f0log2 = log2f(1.0f + 1e-7f);
+    const float rscale = k.opt.ray_scale;
+    const float* fg = k.g.features + (size_t)(active ? gi : 0) * k.g.k_feat;
+
+    float dA[9], dMu[3], dSig = 0.f, dF[kMaxK];
+    for (int t = 0; t < 9; ++t) dA[t] = 0.f;
+    dMu[0] = dMu[1] = dMu[2] = 0.f;
+#pragma unroll
+    for (int t = 0; t < kMaxK; ++t) dF[t] = 0.f;
+    Pair P;
+    float mu[3] = {0.f, 0.f, 0.f};
+    P.i0 = P.i1 = P.j0 = P.j1 = 0;
+    if (active) load_rec(srec[lane], P, mu);
+
+    for (int p = pbeg + wave; p < pend; p += kWaves) {
+        // stage this wall point's upstream gradient row and tables (wave-private)
+        const float hs = k.geo.hscale[p];
+        for (int t = lane; t < nr; t += 64) {
+            const float g = k.grad_hist ? k.grad_hist[(size_t)p * nr + t] : 0.f;
+            grow[t] = g * k.geo.att[t] * hs;
+        }
+        for (int t = lane; t < nt; t += 64)
+            tth[t] = make_float2(k.geo.sin_theta[(size_t)p * nt + t], k.geo.cos_theta[(size_t)p * nt + t]);
+        for (int t = lane; t < np_; t += 64)
+            tph[t] = make_float2(k.geo.cos_phi[(size_t)p * np_ + t], k.geo.sin_phi[(size_t)p * np_ + t]);
+        const float px = k.geo.wall[3 * p], py = k.geo.wall[3 * p + 1], pz = k.geo.wall[3 * p + 2];
+        bool more = false;
+        if (active) {
+            pair_setup<PRESET, DENSE>(k, gi, mu, px, py, pz, k.geo.grid_lin + 4 * (size_t)p, mc2, P);
+            more = (P.w > 0.f) && P.i0 <= P.i1 && P.j0 <= P.j1;
+            pd[lane] = make_float4(P.u0[0], P.u0[1], P.u0[2], P.w);
+            prho[lane] = P.rho;
+        }
+        const float* gray = RAYS && k.grad_ray ? k.grad_ray + (size_t)p * nt * np_ * nr : nullptr;
+        wave_sync();
+        int ci = P.i0, cj = P.j0;
+        int cnt = 0;
+        while (__builtin_amdgcn_ballot_w64(more)) {
+            bool pass = false;
+            uint2 e;
+            if (more) {
+                const float2 th = tth[ci], ph = tph[cj];
+                const float dx = th.x * ph.x, dy = th.x * ph.y, dz = th.y;
+                if (DENSE || quadric(P.M, dx, dy, dz) >= 0.f) {
+                    Ray R;
+                    if (ray_setup<DENSE>(P.A, P.u0, dx, dy, dz, mc2, r0, dr, nr, R)) {
+                        e = make_uint2((unsigned)lane | ((unsigned)ci << 8) | ((unsigned)cj << 20),
+                                       (unsigned)R.kl | ((unsigned)R.kh << 16));
+                        pass = true;
+                    }
+                }
+                if (++cj > P.j1) { cj = P.j0; ++ci; }
+                more = ci <= P.i1;
+            }
+            const unsigned long long m = __builtin_amdgcn_ballot_w64(pass);
+            if (pass) queue[cnt + lanes_below(m)] = e;
+            cnt += __popcll(m);
+            if (cnt >= 64) {
+                wave_sync();
+                bwd_drain<MODE, RAYS>(srec, grow, tth, tph, pd, prho, pacc, queue, 64, gray, np_, r0, dr, nr, cdt,
+                                      f0log2, rscale);
+                wave_sync();
+                if (lane < cnt - 64) queue[lane] = queue[64 + lane];
+                wave_sync();
+                cnt -= 64;
+            }
+        }
+        wave_sync();
+        bwd_drain<MODE, RAYS>(srec, grow, tth, tph, pd, prho, pacc, queue, cnt, gray, np_, r0, dr, nr, cdt, f0log2,
+                              rscale);
+        wave_sync();
+        // per-pair chain for this wave's pair (Gaussian gi, wall point p)
+        if (active) {
+            float* pa = pacc + lane * 16;
+            const float dU0[3] = {pa[0], pa[1], pa[2]};
+            for (int r = 0; r < 3; ++r) {  // u0 = A (p - mu)
+                dA[3 * r] += pa[3 + 3 * r] + dU0[r] * P.q[0];
+                dA[3 * r + 1] += pa[4 + 3 * r] + dU0[r] * P.q[1];
+                dA[3 * r + 2] += pa[5 + 3 * r] + dU0[r] * P.q[2];
+            }
+            for (int c = 0; c < 3; ++c) dMu[c] -= P.A[c] * dU0[0] + P.A[3 + c] * dU0[1] + P.A[6 + c] * dU0[2];
+            dSig += pa[12];
+            const float drho = pa[13];
+            for (int t = 0; t < 16; ++t) pa[t] = 0.f;
+            // rho = max(0, 0.5 + sum_c f_c Y_c(dir)); torch's clamp_min passes the gradient at equality
+            if (P.w > 0.f && P.sh + 0.5f >= 0.f && drho != 0.f) {
+                float Y[kMaxK];
+                sh_basis<PRESET>(deg, P.dir[0], P.dir[1], P.dir[2], Y);
+#pragma unroll
+                for (int c = 0; c < kMaxK; ++c)
+                    if (c < K) dF[c] += drho * Y[c];
+                float gx, gy, gz;
+                sh_grad_dir<PRESET>(deg, P.dir[0], P.dir[1], P.dir[2], fg, gx, gy, gz);
+                float ox, oy, oz;
+                view_dir_bwd<PRESET>(-P.q[0], -P.q[1], -P.q[2], P.nrm, drho * gx, drho * gy, drho * gz, ox, oy, oz);
+                dMu[0] += ox; dMu[1] += oy; dMu[2] += oz;
+            }
+        }
+        wave_sync();
+    }
+    // fixed-order combination of the 4 waves' accumulators -> partial slab
+    __syncthreads();
+    float* red = smem + L.red;
+    {
+        float* dst = red + (wave * 64 + lane) * 29;
+        for (int t = 0; t < 9; ++t) dst[t] = dA[t];
+        dst[9] = dMu[0]; dst[10] = dMu[1]; dst[11] = dMu[2];
+        dst[12] = dSig;
+#pragma unroll
+        for (int t = 0; t < kMaxK; ++t) dst[13 + t] = dF[t];
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < kNB * 29; t += blockDim.x) {
+        const int g = t / 29, c = t - g * 29;
+        if (gb + g >= k.g.ng) continue;
+        float s = 0.f;
+        for (int w = 0; w < kWaves; ++w) s += red[(w * 64 + g) * 29 + c];
+        k.partial[((size_t)split * k.g.ng + gb + g) * 32 + c] = s;
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// finish: reduce the splits and chain dA / dsigma to the raw parameters
+// ------------------------------------------------------------------------------------------
+template <int PRESET>
+__global__ __launch_bounds__(kBlock) void finish_kernel(KArgs k, float* d_mu, float* d_scaling, float* d_rot,
+                                                        float* d_opac, float* d_feat) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= k.g.ng) return;
+    float acc[32];
+    for (int t = 0; t < 32; ++t) acc[t] = 0.f;
+    for (int s = 0; s < k.nsplit; ++s) {
+        const float* src = k.partial + ((size_t)s * k.g.ng + i) * 32;
+        for (int t = 0; t < 29; ++t) acc[t] += src[t];
+    }
+    const float* S = k.g.scaling + 3 * i;
+    const float* Q = k.g.rotation + 4 * i;
+    const float O = k.g.opacity[i];
+    const float mod = k.g.scaling_modifier;
+    GaussAct a;
+    activate<PRESET>(S, Q, O, mod, a);
+    // A_rc = R'_rc / s~_r
+    float dRp[9], dst[3];
+    for (int r = 0; r < 3; ++r) {
+        float acc_s = 0.f;
+        for (int c = 0; c < 3; ++c) {
+            dRp[3 * r + c] = acc[3 * r + c] / a.st[r];
+            acc_s += acc[3 * r + c] * a.Rp[3 * r + c];
+        }
+        dst[r] = -acc_s / (a.st[r] * a.st[r]);
+    }
+    float dR[9];
+    if (PRESET == NLOSGR_PRESET_TORCH) {
+        for (int t = 0; t < 9; ++t) dR[t] = dRp[t];
+        for (int r = 0; r < 3; ++r) {
+            const float e = expf(S[r]) * mod;     // s = exp(e), ds/dS = s * e
+            d_scaling[3 * i + r] = dst[r] * a.st[r] * e;
+        }
+        // q^ = Q / max(|Q|,1e-12); qn = q^/|q^|; R = R(qn)
+        const float n0 = sqrtf(Q[0] * Q[0] + Q[1] * Q[1] + Q[2] * Q[2] + Q[3] * Q[3]);
+        const float d0 = fmaxf(n0, 1e-12f);
+        float qh[4] = {Q[0] / d0, Q[1] / d0, Q[2] / d0, Q[3] / d0};
+        const float n1 = sqrtf(qh[0] * qh[0] + qh[1] * qh[1] + qh[2] * qh[2] + qh[3] * qh[3]);
+        float qn[4] = {qh[0] / n1, qh[1] / n1, qh[2] / n1, qh[3] / n1};
+        float dqn[4];
+        quat_rot_bwd(qn[0], qn[1], qn[2], qn[3], dR, dqn[0], dqn[1], dqn[2], dqn[3]);
+        float dp = qn[0] * dqn[0] + qn[1] * dqn[1] + qn[2] * dqn[2] + qn[3] * dqn[3];
+        float dqh[4];
+        for (int t = 0; t < 4; ++t) dqh[t] = (dqn[t] - qn[t] * dp) / n1;
+        if (n0 > 1e-12f) {
+            float dp2 = qh[0] * dqh[0] + qh[1] * dqh[1] + qh[2] * dqh[2] + qh[3] * dqh[3];
+            for (int t = 0; t < 4; ++t) d_rot[4 * i + t] = (dqh[t] - qh[t] * dp2) / n0;
+        } else {
+            for (int t = 0; t < 4; ++t) d_rot[4 * i + t] = dqh[t] / d0;
+        }
+    } else {
+        // R' = R^T
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 3; ++c) dR[3 * c + r] = dRp[3 * r + c];
+        for (int r = 0; r < 3; ++r) d_scaling[3 * i + r] = dst[r] * (a.st[r] - 1e-8f);  // s = exp(S) mod
+        const float n = sqrtf(Q[0] * Q[0] + Q[1] * Q[1] + Q[2] * Q[2] + Q[3] * Q[3]);
+        if (n < 1e-8f) {
+            for (int t = 0; t < 4; ++t) d_rot[4 * i + t] = 0.f;
+        } else {
+            float qn[4] = {Q[0] / n, Q[1] / n, Q[2] / n, Q[3] / n};
+            float dqn[4];
+            quat_rot_bwd(qn[0], qn[1], qn[2], qn[3], dR, dqn[0], dqn[1], dqn[2], dqn[3]);
+            float dp = qn[0] * dqn[0] + qn[1] * dqn[1] + qn[2] * dqn[2] + qn[3] * dqn[3];
+            for (int t = 0; t < 4; ++t) d_rot[4 * i + t] = (dqn[t] - qn[t] * dp) / n;
+        }
+    }
+    d_mu[3 * i] = acc[9]; d_mu[3 * i + 1] = acc[10]; d_mu[3 * i + 2] = acc[11];
+    d_opac[i] = acc[12] * a.sigma * (1.0f - a.sigma);
+    const int kf = k.g.k_feat;
+    const int K = (k.g.sh_degree + 1) * (k.g.sh_degree + 1);
+#pragma unroll
+    for (int c = 0; c < kMaxK; ++c)
+        if (c < kf) d_feat[(size_t)i * kf + c] = c < K ? acc[13 + c] : 0.f;
+}
+
+
+// 3-sigma AABB: bbox_compute.cuh:23-71 (cuda) / gaussian_model.py:140-178 (torch; clamp 1e-8)
+template <int PRESET>
+__global__ __launch_bounds__(kBlock) void bbox_kernel(nlosgr_gaussians g, float sig, float* out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= g.ng) return;
+    float s[3];
+    for (int t = 0; t < 3; ++t) s[t] = expf(g.scaling[3 * i + t]) * g.scaling_modifier;
+    const float* Q = g.rotation + 4 * i;
+    float n = sqrtf(Q[0] * Q[0] + Q[1] * Q[1] + Q[2] * Q[2] + Q[3] * Q[3]);
+    float R[9];
+    if (PRESET == NLOSGR_PRESET_CUDA && n < 1e-8f) {
+        R[0] = 1.f; R[1] = 0.f; R[2] = 0.f; R[3] = 0.f; R[4] = 1.f; R[5] = 0.f; R[6] = 0.f; R[7] = 0.f; R[8] = 1.f;
+    } else {
+        if (PRESET == NLOSGR_PRESET_TORCH) n = fmaxf(n, 1e-12f);
+        float q[4] = {Q[0] / n, Q[1] / n, Q[2] / n, Q[3] / n};
+        if (PRESET == NLOSGR_PRESET_TORCH) {
+            float n1 = sqrtf(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+            for (int t = 0; t < 4; ++t) q[t] /= n1;
+        }
+        quat_rot(q[0], q[1], q[2], q[3], R);
+    }
+    for (int r = 0; r < 3; ++r) {
+        float v = 0.f;
+        for (int c = 0; c < 3; ++c) v += (R[3 * r + c] * s[c]) * (R[3 * r + c] * s[c]);
+        if (PRESET == NLOSGR_PRESET_TORCH) v = fmaxf(v, 1e-8f);
+        const float e = sig * sqrtf(v);
+        out[6 * i + r] = g.mu[3 * i + r] - e;
+        out[6 * i + 3 + r] = g.mu[3 * i + r] + e;
+    }
+}
+
+
+// ------------------------------------------------------------------------------------------
+// host side
+// ------------------------------------------------------------------------------------------
+size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
+
+int validate(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_options* opt) {
+    if (!g || !geo || !opt) return set_err(NLOSGR_E_INVALID, "null argument struct");
+    if (g->ng < 0) return set_err(NLOSGR_E_INVALID, "ng must be >= 0");
+    if (g->preset != NLOSGR_PRESET_TORCH && g->preset != NLOSGR_PRESET_CUDA)
+        return set_err(NLOSGR_E_INVALID, "unknown preset");
+    if (g->sh_degree < 0 || g->sh_degree > 3)
+        return set_err(NLOSGR_E_UNSUPPORTED, "active_sh_degree must be in [0, 3]");
+    if (g->k_feat < (g->sh_degree + 1) * (g->sh_degree + 1) || g->k_feat > kMaxK)
+        return set_err(NLOSGR_E_INVALID, "k_feat must satisfy (sh_degree+1)^2 <= k_feat <= 16");
+    if (opt->mode != NLOSGR_MODE_NOOCL && opt->mode != NLOSGR_MODE_NETF)
+        return set_err(NLOSGR_E_INVALID, "unknown mode");
+    if (geo->nwall < 0 || geo->nt < 1 || geo->np < 1 || geo->nr < 1)
+        return set_err(NLOSGR_E_INVALID, "bad geometry sizes");
+    if (geo->nr > 4096 || geo->nt > 1024 || geo->np > 1024)
+        return set_err(NLOSGR_E_UNSUPPORTED, "nr <= 4096 and nt, np <= 1024");
+    if (g->ng > 0 && (!g->mu || !g->scaling || !g->rotation || !g->opacity || !g->features))
+        return set_err(NLOSGR_E_INVALID, "null Gaussian parameter pointer");
+    if (geo->nwall > 0 && (!geo->wall || !geo->sin_theta || !geo->cos_theta || !geo->sin_phi ||
+                           !geo->cos_phi || !geo->grid_lin || !geo->hscale || !geo->r || !geo->att))
+        return set_err(NLOSGR_E_INVALID, "null geometry pointer");
+    const size_t lds_f = (size_t)FwdLayout(geo->nr, geo->nt, geo->np).total * 4;
+    const size_t lds_b = (size_t)BwdLayout(geo->nr, geo->nt, geo->np).total * 4;
+    if (lds_f > 160 * 1024 || lds_b > 160 * 1024) return set_err(NLOSGR_E_UNSUPPORTED, "problem exceeds LDS budget");
+    return NLOSGR_OK;
+}
+
+int bwd_nsplit(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_options* opt) {
+    const int maxs = geo->nwall > 0 ? geo->nwall : 1;
+    if (opt->nsplit > 0) return opt->nsplit < maxs ? opt->nsplit : maxs;
+    const int nblk = (g->ng + kNB - 1) / kNB;
+    int ns = (2048 + nblk - 1) / (nblk > 0 ? nblk : 1);  // aim for >= 2048 workgroups (8 per CU)
+    if (ns > maxs) ns = maxs;
+    if (ns < 1) ns = 1;
+    return ns;
+}
+
+#define HIPCHK(x)                                                                  \
+    do {                                                                           \
+        hipError_t e_ = (x);                                                       \
+        if (e_ != hipSuccess) return set_err(NLOSGR_E_HIP, hipGetErrorString(e_)); \
+    } while (0)
+
+template <int PRESET, int MODE, bool DENSE, bool RAYS>
+void launch_fwd(const KArgs& ka, size_t shm, hipStream_t s) {
+    hipLaunchKernelGGL((fwd_kernel<PRESET, MODE, DENSE, RAYS>), dim3(ka.geo.nwall), dim3(kBlock), shm, s, ka);
+}
+template <int PRESET, int MODE, bool DENSE, bool RAYS>
+void launch_bwd(const KArgs& ka, size_t shm, hipStream_t s) {
+    dim3 grid((ka.g.ng + kNB - 1) / kNB, ka.nsplit);
+    hipLaunchKernelGGL((bwd_kernel<PRESET, MODE, DENSE, RAYS>), grid, dim3(kBlock), shm, s, ka);
+}
+
+template <int PRESET, int MODE>
+void dispatch_fwd(const KArgs& ka, bool dense, bool rays, size_t shm, hipStream_t s) {
+    if (dense) {
+        if (rays) launch_fwd<PRESET, MODE, true, true>(ka, shm, s);
+        else launch_fwd<PRESET, MODE, true, false>(ka, shm, s);
+    } else {
+        if (rays) launch_fwd<PRESET, MODE, false, true>(ka, shm, s);
+        else launch_fwd<PRESET, MODE, false, false>(ka, shm, s);
+    }
+}
+template <int PRESET, int MODE>
+void dispatch_bwd(const KArgs& ka, bool dense, bool rays, size_t shm, hipStream_t s) {
+    if (dense) {
+        if (rays) launch_bwd<PRESET, MODE, true, true>(ka, shm, s);
+        else launch_bwd<PRESET, MODE, true, false>(ka, shm, s);
+    } else {
+        if (rays) launch_bwd<PRESET, MODE, false, true>(ka, shm, s);
+        else launch_bwd<PRESET, MODE, false, false>(ka, shm, s);
+    }
+}
+
+void launch_preprocess(const nlosgr_gaussians* g, GaussRec* recs, hipStream_t s) {
+    const int nb = (g->ng + kBlock - 1) / kBlock;
+    if (g->preset == NLOSGR_PRESET_TORCH)
+        hipLaunchKernelGGL(preprocess_kernel<NLOSGR_PRESET_TORCH>, dim3(nb), dim3(kBlock), 0, s, *g, recs);
+    else
+        hipLaunchKernelGGL(preprocess_kernel<NLOSGR_PRESET_CUDA>, dim3(nb), dim3(kBlock), 0, s, *g, recs);
+}
+
+}  // namespace
+
+extern "C" {
+
+int nlosgr_abi_version(void) { return NLOSGR_ABI_VERSION; }
+
+const char* nlosgr_last_error(void) { return g_err; }
+
+size_t nlosgr_workspace_bytes(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_options* opt) {
+    if (validate(g, geo, opt) != NLOSGR_OK) return 0;
+    const size_t rec = align_up((size_t)g->ng * sizeof(GaussRec));
+    const size_t part = align_up((size_t)bwd_nsplit(g, geo, opt) * g->ng * 32 * sizeof(float));
+    return rec + part + 256;
+}
+
+int nlosgr_render_fwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_options* opt,
+                      void* workspace, float* hist_out, float* ray_out, void* hip_stream) {
+    int rc = validate(g, geo, opt);
+    if (rc) return rc;
+    if (geo->nwall == 0 || (!hist_out && !ray_out)) return NLOSGR_OK;
+    if (g->ng > 0 && !workspace) return set_err(NLOSGR_E_INVALID, "workspace is null");
+    hipStream_t s = (hipStream_t)hip_stream;
+    KArgs ka;
+    memset(&ka, 0, sizeof(ka));
+    ka.g = *g; ka.geo = *geo; ka.opt = *opt;
+    ka.recs = (const GaussRec*)workspace;
+    ka.hist_out = hist_out; ka.ray_out = ray_out;
+    if (g->ng > 0) {
+        launch_preprocess(g, (GaussRec*)workspace, s);
+        HIPCHK(hipGetLastError());
+    }
+    const size_t shm = (size_t)FwdLayout(geo->nr, geo->nt, geo->np).total * sizeof(float);
+    const bool dense = !(opt->cutoff > 0.f);
+    const bool rays = ray_out != nullptr;
+    if (g->preset == NLOSGR_PRESET_TORCH) {
+        if (opt->mode == NLOSGR_MODE_NOOCL) dispatch_fwd<0, 0>(ka, dense, rays, shm, s);
+        else dispatch_fwd<0, 1>(ka, dense, rays, shm, s);
+    } else {
+        if (opt->mode == NLOSGR_MODE_NOOCL) dispatch_fwd<1, 0>(ka, dense, rays, shm, s);
+        else dispatch_fwd<1, 1>(ka, dense, rays, shm, s);
+    }
+    HIPCHK(hipGetLastError());
+    return NLOSGR_OK;
+}
+
+int nlosgr_render_bwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_options* opt,
+                      void* workspace, const float* grad_hist, const float* grad_ray, float* d_mu,
+                      float* d_scaling, float* d_rotation, float* d_opacity, float* d_features,
+                      void* hip_stream) {
+    int rc = validate(g, geo, opt);
+    if (rc) return rc;
+    if (g->ng == 0) return NLOSGR_OK;
+    if (!workspace) return set_err(NLOSGR_E_INVALID, "workspace is null");
+    if (!d_mu || !d_scaling || !d_rotation || !d_opacity || !d_features)
+        return set_err(NLOSGR_E_INVALID, "null gradient output pointer");
+    hipStream_t s = (hipStream_t)hip_stream;
+    KArgs ka;
+    memset(&ka, 0, sizeof(ka));
+    ka.g = *g; ka.geo = *geo; ka.opt = *opt;
+    ka.recs = (const GaussRec*)workspace;
+    ka.partial = (float*)((char*)workspace + align_up((size_t)g->ng * sizeof(GaussRec)));
+    ka.grad_hist = grad_hist; ka.grad_ray = grad_ray;
+    ka.nsplit = bwd_nsplit(g, geo, opt);
+    launch_preprocess(g, (GaussRec*)workspace, s);
+    HIPCHK(hipGetLastError());
+    if (geo->nwall > 0 && (grad_hist || grad_ray)) {
+        const size_t shm = (size_t)BwdLayout(geo->nr, geo->nt, geo->np).total * sizeof(float);
+        const bool dense = !(opt->cutoff > 0.f);
+        const bool rays = grad_ray != nullptr;
+        if (g->preset == NLOSGR_PRESET_TORCH) {
+            if (opt->mode == NLOSGR_MODE_NOOCL) dispatch_bwd<0, 0>(ka, dense, rays, shm, s);
+            else dispatch_bwd<0, 1>(ka, dense, rays, shm, s);
+        } else {
+            if (opt->mode == NLOSGR_MODE_NOOCL) dispatch_bwd<1, 0>(ka, dense, rays, shm, s);
+            else dispatch_bwd<1, 1>(ka, dense, rays, shm, s);
+        }
+        HIPCHK(hipGetLastError());
+    } else {
+        HIPCHK(hipMemsetAsync(ka.partial, 0, (size_t)ka.nsplit * g->ng * 32 * sizeof(float), s));
+    }
+    const int nb = (g->ng + kBlock - 1) / kBlock;
+    if (g->preset == NLOSGR_PRESET_TORCH)
+        hipLaunchKernelGGL(finish_kernel<NLOSGR_PRESET_TORCH>, dim3(nb), dim3(kBlock), 0, s, ka, d_mu, d_scaling,
+                           d_rotation, d_opacity, d_features);
+    else
+        hipLaunchKernelGGL(finish_kernel<NLOSGR_PRESET_CUDA>, dim3(nb), dim3(kBlock), 0, s, ka, d_mu, d_scaling,
+                           d_rotation, d_opacity, d_features);
+    HIPCHK(hipGetLastError());
+    return NLOSGR_OK;
+}
+
+int nlosgr_bboxes(const nlosgr_gaussians* g, float sigma_scale, float* bboxes_out, void* hip_stream) {
+    if (!g || !bboxes_out) return set_err(NLOSGR_E_INVALID, "null argument");
+    if (g->ng <= 0) return NLOSGR_OK;
+    hipStream_t s = (hipStream_t)hip_stream;
+    const int nb = (g->ng + kBlock - 1) / kBlock;
+    if (g->preset == NLOSGR_PRESET_TORCH)
+        hipLaunchKernelGGL(bbox_kernel<NLOSGR_PRESET_TORCH>, dim3(nb), dim3(kBlock), 0, s, *g, sigma_scale, bboxes_out);
+    else
+        hipLaunchKernelGGL(bbox_kernel<NLOSGR_PRESET_CUDA>, dim3(nb), dim3(kBlock), 0, s, *g, sigma_scale, bboxes_out);
+    HIPCHK(hipGetLastError());
+    return NLOSGR_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,98 @@
+"""ctypes binding of the C ABI in include/nlosgr.h (libnlosgr.so, built in-tree for gfx950).
+
+There is no CPU fallback: if the library is missing or no GPU is visible, every render call
+raises.  torch is imported first so the library binds to the HIP runtime torch loaded.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (must precede the ctypes load: shared libamdhip64.so.7)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libnlosgr.so")
+
+PRESET_TORCH = 0
+PRESET_CUDA = 1
+MODE_NOOCL = 0
+MODE_NETF = 1
+PRESETS = {"torch": PRESET_TORCH, "cuda": PRESET_CUDA}
+MODES = {"noocl": MODE_NOOCL, "netf": MODE_NETF}
+
+_P = ctypes.c_void_p
+
+
+class Gaussians(ctypes.Structure):
+    _fields_ = [("ng", ctypes.c_int32), ("k_feat", ctypes.c_int32), ("sh_degree", ctypes.c_int32),
+                ("preset", ctypes.c_int32), ("scaling_modifier", ctypes.c_float),
+                ("mu", _P), ("scaling", _P), ("rotation", _P), ("opacity", _P), ("features", _P)]
+
+
+class Geometry(ctypes.Structure):
+    _fields_ = [("nwall", ctypes.c_int32), ("nt", ctypes.c_int32), ("np", ctypes.c_int32),
+                ("nr", ctypes.c_int32), ("wall", _P), ("sin_theta", _P), ("cos_theta", _P),
+                ("sin_phi", _P), ("cos_phi", _P), ("grid_lin", _P), ("hscale", _P), ("r", _P),
+                ("att", _P)]
+
+
+class Options(ctypes.Structure):
+    _fields_ = [("mode", ctypes.c_int32), ("cutoff", ctypes.c_float), ("c_deltaT", ctypes.c_float),
+                ("ray_scale", ctypes.c_float), ("nsplit", ctypes.c_int32), ("flags", ctypes.c_int32)]
+
+
+# every symbol include/nlosgr.h declares (tests check the exports against this list)
+EXPORTS = ["nlosgr_workspace_bytes", "nlosgr_render_fwd", "nlosgr_render_bwd", "nlosgr_bboxes",
+           "nlosgr_last_error", "nlosgr_abi_version"]
+
+_lib = None
+_load_error = None
+
+
+def load():
+    """Load (once) and return the library; raises if it is missing."""
+    global _lib, _load_error
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"nlosgr: HIP library not built: {LIB_PATH} "
+                           "(run python nlos-gaussian-renderer_amd/build.py)")
+    lib = ctypes.CDLL(LIB_PATH)
+    PG, PGEO, POPT = ctypes.POINTER(Gaussians), ctypes.POINTER(Geometry), ctypes.POINTER(Options)
+    lib.nlosgr_workspace_bytes.argtypes = [PG, PGEO, POPT]
+    lib.nlosgr_workspace_bytes.restype = ctypes.c_size_t
+    lib.nlosgr_render_fwd.argtypes = [PG, PGEO, POPT, _P, _P, _P, _P]
+    lib.nlosgr_render_fwd.restype = ctypes.c_int
+    lib.nlosgr_render_bwd.argtypes = [PG, PGEO, POPT, _P, _P, _P, _P, _P, _P, _P, _P, _P]
+    lib.nlosgr_render_bwd.restype = ctypes.c_int
+    lib.nlosgr_bboxes.argtypes = [PG, ctypes.c_float, _P, _P]
+    lib.nlosgr_bboxes.restype = ctypes.c_int
+    lib.nlosgr_last_error.argtypes = []
+    lib.nlosgr_last_error.restype = ctypes.c_char_p
+    lib.nlosgr_abi_version.argtypes = []
+    lib.nlosgr_abi_version.restype = ctypes.c_int
+    if lib.nlosgr_abi_version() != 1:
+        raise RuntimeError("nlosgr: ABI version mismatch")
+    _lib = lib
+    return lib
+
+
+def available():
+    """True when the library loads and a GPU is visible (CUDA_AVAILABLE of the reference API)."""
+    try:
+        load()
+    except Exception:
+        return False
+    return torch.cuda.is_available()
+
+
+def check(rc):
+    if rc != 0:
+        msg = load().nlosgr_last_error().decode(errors="replace")
+        raise RuntimeError(f"nlosgr error {rc}: {msg}")
+
+
+def ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def stream_handle(device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)

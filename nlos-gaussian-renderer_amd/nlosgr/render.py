@@ -1,0 +1,134 @@
+"""Autograd Function over the C ABI (nlosgr_render_fwd / nlosgr_render_bwd).
+
+RenderFn is the single differentiable entry point everything else (the reference-API mirrors,
+the batched volume renderer, the multi-GPU shard) is built on.  It returns
+    hist [P, nr]              hscale[p] * att[k] * sum_{g,ij} w_g(p) sin(theta_i) pdf
+    rays [P, nt*np, nr]       ray_scale * sum_g w_g(p) pdf           (optional; the reference's
+                              per-(ray, sample) layout, rays in meshgrid('ij') order)
+and backward yields real gradients for the five raw parameter tensors (the reference's
+CUDA backward returns zeros, gaussian_model/cuda_autograd.py:147-156).
+"""
+from dataclasses import dataclass
+
+import torch
+
+from . import _lib
+
+
+@dataclass(frozen=True)
+class RenderConfig:
+    preset: str = "torch"        # "torch" (path T) or "cuda" (path C)
+    mode: str = "noocl"          # "noocl" or "netf"
+    sh_degree: int = 0
+    scaling_modifier: float = 1.0
+    cutoff: float = 0.0          # Mahalanobis support radius; <= 0 -> dense
+    c_deltaT: float = 1.0
+    ray_scale: float = 1.0
+    nsplit: int = 0
+
+
+def _as_f32(t):
+    t = t.detach()
+    if t.dtype != torch.float32:
+        raise TypeError(f"nlosgr: expected float32 tensor, got {t.dtype}")
+    if not t.is_cuda:
+        raise RuntimeError("nlosgr: tensors must live on the GPU (no CPU fallback)")
+    return t.contiguous()
+
+
+def _structs(mu, scaling, rotation, opacity, features, geo, cfg):
+    ng = mu.shape[0]
+    k_feat = features.shape[1] if features.dim() == 2 else 0
+    if mu.shape != (ng, 3) or scaling.shape != (ng, 3) or rotation.shape != (ng, 4):
+        raise ValueError("nlosgr: mu/scaling must be [Ng,3] and rotation [Ng,4]")
+    if opacity.numel() != ng or features.shape[0] != ng or features.dim() != 2:
+        raise ValueError("nlosgr: opacity must have Ng elements and features be [Ng,K]")
+    g = _lib.Gaussians(ng, k_feat, int(cfg.sh_degree), _lib.PRESETS[cfg.preset],
+                       float(cfg.scaling_modifier), _lib.ptr(mu), _lib.ptr(scaling), _lib.ptr(rotation),
+                       _lib.ptr(opacity), _lib.ptr(features))
+    gs = _lib.Geometry(geo.nwall, geo.nt, geo.np, geo.nr, _lib.ptr(geo.wall), _lib.ptr(geo.sin_theta),
+                       _lib.ptr(geo.cos_theta), _lib.ptr(geo.sin_phi), _lib.ptr(geo.cos_phi),
+                       _lib.ptr(geo.grid_lin), _lib.ptr(geo.hscale), _lib.ptr(geo.r), _lib.ptr(geo.att))
+    o = _lib.Options(_lib.MODES[cfg.mode], float(cfg.cutoff), float(cfg.c_deltaT), float(cfg.ray_scale),
+                     int(cfg.nsplit), 0)
+    return g, gs, o
+
+
+def _workspace(lib, g, gs, o, device):
+    nbytes = lib.nlosgr_workspace_bytes(g, gs, o)
+    if nbytes == 0:
+        _lib.check(1)
+    return torch.empty(nbytes, dtype=torch.uint8, device=device)
+
+
+def render_forward(mu, scaling, rotation, opacity, features, geo, cfg, want_hist=True, want_rays=False):
+    """Non-differentiable forward (used by RenderFn and by inference callers)."""
+    lib = _lib.load()
+    dev = mu.device
+    mu, scaling, rotation, opacity, features = [_as_f32(t) for t in (mu, scaling, rotation, opacity, features)]
+    g, gs, o = _structs(mu, scaling, rotation, opacity, features, geo, cfg)
+    ws = _workspace(lib, g, gs, o, dev)
+    hist = torch.empty(geo.nwall, geo.nr, device=dev) if want_hist else None
+    rays = torch.zeros(geo.nwall, geo.nt * geo.np, geo.nr, device=dev) if want_rays else None
+    _lib.check(lib.nlosgr_render_fwd(g, gs, o, _lib.ptr(ws), _lib.ptr(hist), _lib.ptr(rays),
+                                     _lib.stream_handle(dev)))
+    return hist, rays
+
+
+def render_backward(mu, scaling, rotation, opacity, features, geo, cfg, grad_hist=None, grad_rays=None):
+    lib = _lib.load()
+    dev = mu.device
+    mu, scaling, rotation, opacity, features = [_as_f32(t) for t in (mu, scaling, rotation, opacity, features)]
+    g, gs, o = _structs(mu, scaling, rotation, opacity, features, geo, cfg)
+    ws = _workspace(lib, g, gs, o, dev)
+    gh = grad_hist.float().contiguous() if grad_hist is not None else None
+    gr = grad_rays.float().contiguous() if grad_rays is not None else None
+    d_mu = torch.empty_like(mu)
+    d_s = torch.empty_like(scaling)
+    d_q = torch.empty_like(rotation)
+    d_o = torch.empty(mu.shape[0], device=dev)
+    d_f = torch.empty_like(features)
+    _lib.check(lib.nlosgr_render_bwd(g, gs, o, _lib.ptr(ws), _lib.ptr(gh), _lib.ptr(gr), _lib.ptr(d_mu),
+                                     _lib.ptr(d_s), _lib.ptr(d_q), _lib.ptr(d_o), _lib.ptr(d_f),
+                                     _lib.stream_handle(dev)))
+    return d_mu, d_s, d_q, d_o, d_f
+
+
+class RenderFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, mu, scaling, rotation, opacity, features, geo, cfg, want_hist, want_rays):
+        hist, rays = render_forward(mu, scaling, rotation, opacity, features, geo, cfg, want_hist, want_rays)
+        ctx.save_for_backward(mu, scaling, rotation, opacity, features)
+        ctx.geo, ctx.cfg, ctx.oshape = geo, cfg, opacity.shape
+        outs = (hist if hist is not None else torch.zeros(0, device=mu.device),
+                rays if rays is not None else torch.zeros(0, device=mu.device))
+        return outs
+
+    @staticmethod
+    def backward(ctx, g_hist, g_rays):
+        mu, scaling, rotation, opacity, features = ctx.saved_tensors
+        gh = g_hist if (g_hist is not None and g_hist.numel() > 0) else None
+        gr = g_rays if (g_rays is not None and g_rays.numel() > 0) else None
+        d_mu, d_s, d_q, d_o, d_f = render_backward(mu, scaling, rotation, opacity, features, ctx.geo, ctx.cfg,
+                                                   gh, gr)
+        return d_mu, d_s, d_q, d_o.reshape(ctx.oshape), d_f, None, None, None, None
+
+
+def render(mu, scaling, rotation, opacity, features, geo, cfg, want_hist=True, want_rays=False):
+    """Differentiable render; returns (hist or None, rays or None)."""
+    hist, rays = RenderFn.apply(mu, scaling, rotation, opacity, features, geo, cfg, want_hist, want_rays)
+    return (hist if want_hist else None), (rays if want_rays else None)
+
+
+def bboxes(mu, scaling, rotation, scaling_modifier=1.0, sigma_scale=3.0, preset="cuda"):
+    """[Ng, 2, 3] axis-aligned sigma_scale boxes (GaussianModel.get_bboxes layout,
+    gaussian_model.py:140-178; bbox_compute.cuh:76-120)."""
+    lib = _lib.load()
+    mu, scaling, rotation = [_as_f32(t) for t in (mu, scaling, rotation)]
+    ng = mu.shape[0]
+    dummy = torch.zeros(ng, device=mu.device)
+    g = _lib.Gaussians(ng, 1, 0, _lib.PRESETS[preset], float(scaling_modifier), _lib.ptr(mu), _lib.ptr(scaling),
+                       _lib.ptr(rotation), _lib.ptr(dummy), _lib.ptr(dummy))
+    out = torch.empty(ng, 6, device=mu.device)
+    _lib.check(lib.nlosgr_bboxes(g, float(sigma_scale), _lib.ptr(out), _lib.stream_handle(mu.device)))
+    return out.view(ng, 2, 3)

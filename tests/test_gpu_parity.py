@@ -1,0 +1,136 @@
+"""GPU parity: the HIP path (through the C ABI) against the reference's golden vectors and the
+CPU oracle.  Tolerances (fp32):
+  forward    max|hip - ref| <= 2e-5 * max|ref| + 1e-7   (dense; summation order differs)
+  gradients  max|hip - ref| <= 2e-4 * max|ref| + 1e-6   per parameter tensor
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import CASES, load_case
+
+pytestmark = pytest.mark.gpu
+
+FWD_RTOL = 2e-5
+GRAD_RTOL = 2e-4
+
+
+def _close(a, b, rtol, atol=1e-7, msg=""):
+    a = np.asarray(a, dtype=np.float64)
+    b = np.asarray(b, dtype=np.float64)
+    scale = np.abs(b).max() if b.size else 0.0
+    err = np.abs(a - b).max() if b.size else 0.0
+    assert err <= rtol * scale + atol, f"{msg}: max err {err:.3e} vs scale {scale:.3e}"
+
+
+def _args(m):
+    from types import SimpleNamespace
+    return SimpleNamespace(num_sampling_points=m["ns"], start=m["start"], end=m["end"], occlusion=m["occlusion"],
+                           rendering_type="netf", scaling_modifier=1.0, gt_times=m["gt_times"])
+
+
+def _model(d, dev):
+    from nlosgr import GaussianParams
+    t = lambda k: torch.from_numpy(d[k]).float().to(dev)
+    return GaussianParams(t("mu"), t("scaling"), t("rotation"), t("opacity"), t("features_dc"),
+                          t("features_rest"), d["meta"]["deg"], d["meta"]["deg"])
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_dropin_matches_reference_golden(name):
+    """nlosgr.nlos_helpers.compute_loss (HIP) vs the reference's compute_loss on the same inputs."""
+    from nlosgr import nlos_helpers as NH
+    dev = torch.device("cuda:0")
+    d = load_case(name)
+    m = d["meta"]
+    model = _model(d, dev)
+    args = _args(m)
+    data_kwargs = {
+        "nlos_data": torch.from_numpy(d["nlos_data"]).to(dev),
+        "camera_grid_positions": torch.from_numpy(d["walls"]).t().contiguous().to(dev),
+        "volume_position": torch.from_numpy(d["volume_position"]).to(dev),
+        "volume_box_point": torch.from_numpy(d["box"]).to(dev),
+        "deltaT": m["deltaT"], "c": m["c"],
+    }
+    crit = torch.nn.MSELoss(reduction="mean")
+    total = 0.0
+    for w in range(m["nwall"]):
+        cam = data_kwargs["camera_grid_positions"][:, w]
+        ip, I1, I2, num_r, dth, dph, *_ = NH.spherical_sample_histogram(args, data_kwargs, cam)
+        assert I1 == d["I1"][w] and I2 == d["I2"][w]
+        result, hist = NH.gaussian_transient_rendering(args, model, data_kwargs, ip, cam, I1, I2, num_r, dth, dph)
+        _close(hist.detach().cpu(), d["hist"][w], FWD_RTOL, msg=f"{name} hist w{w}")
+        _close(result.detach().cpu(), d["result"][w], FWD_RTOL, msg=f"{name} result w{w}")
+        loss, eq = NH.compute_loss(args, model, data_kwargs, {"m": 0, "N": m["nwall"], "n": w, "criterion": crit}, dev)
+        np.testing.assert_allclose(loss.item(), d["loss"][w], rtol=1e-4)
+        total = total + loss
+    total.backward()
+    for pname, leaf in zip(["mu", "scaling", "rotation", "opacity", "features_dc", "features_rest"],
+                           model.parameters()):
+        ref = d["grad_" + pname]
+        if ref.size == 0:
+            continue
+        _close(leaf.grad.cpu(), ref, GRAD_RTOL, atol=1e-6, msg=f"{name} grad {pname}")
+
+
+def _oracle_volume(d_params, walls, box, Y, ns, start, end, c, deltaT, preset, mode, mc, deg):
+    from oracle import torch_ref as R
+    P = R.Params(*d_params, deg)
+    hist = R.render_volume(P, walls, box, Y, ns, start, end, c, deltaT, preset=preset, mode=mode, mc=mc)
+    return P, hist
+
+
+@pytest.mark.parametrize("preset", ["torch", "cuda"])
+@pytest.mark.parametrize("mode", ["noocl", "netf"])
+@pytest.mark.parametrize("cutoff", [0.0, 3.0])
+def test_volume_vs_oracle(preset, mode, cutoff):
+    """Batched volume render (several wall points in one launch) + grads vs the oracle (same
+    Mahalanobis support mask when cutoff > 0)."""
+    from nlosgr import GaussianParams, features_flat
+    from nlosgr.geometry import build_geometry, relay_wall_grid, volume_box_point
+    from nlosgr.render import RenderConfig, render
+    dev = torch.device("cuda:0")
+    ng, deg, ns, T = 48, 3, 6, 40
+    c, deltaT = 1.0, 1.28 / T
+    start, end = T // 8, T // 8 + T
+    model = GaussianParams.synthetic(ng, deg, preset=preset, device=dev, seed=3)
+    if preset == "cuda":   # make them large enough to cross several rays/bins at this coarse grid
+        with torch.no_grad():
+            model._scaling.add_(1.2)
+    walls = relay_wall_grid(2, 3, device=dev)
+    box = volume_box_point((0.0, 0.5, 0.0), 0.5, dev)
+    geo = build_geometry(walls, box, ns, start, end, c, deltaT, 0.5, preset, mode)
+    cfg = RenderConfig(preset=preset, mode=mode, sh_degree=deg, cutoff=cutoff, c_deltaT=c * deltaT)
+    hist, _ = render(model._mu, model._scaling, model._rotation, model._opacity, features_flat(model), geo, cfg)
+    g = torch.Generator().manual_seed(5)
+    gout = torch.randn(hist.shape, generator=g)
+    (hist * gout.to(dev)).sum().backward()
+
+    cpu = lambda t: t.detach().cpu()
+    params = [cpu(model._mu), cpu(model._scaling), cpu(model._rotation), cpu(model._opacity),
+              cpu(model._features_dc), cpu(model._features_rest)]
+    P, ref = _oracle_volume(params, cpu(walls), cpu(box), 0.5, ns, start, end, c, deltaT, preset, mode,
+                            cutoff if cutoff > 0 else None, deg)
+    _close(cpu(hist), ref.detach(), FWD_RTOL, msg="hist")
+    (ref * gout).sum().backward()
+    for pname, leaf, rleaf in zip(["mu", "scaling", "rotation", "opacity", "dc", "rest"], model.parameters(),
+                                  P.leaves()):
+        _close(cpu(leaf.grad), rleaf.grad, GRAD_RTOL, atol=1e-6, msg=f"grad {pname}")
+
+
+def test_cutoff_converges_to_dense():
+    """Support culling error shrinks with the cutoff (cuda preset, physically sized Gaussians)."""
+    from nlosgr import GaussianParams
+    from nlosgr.volume import Scene, make_config, render_volume
+    dev = torch.device("cuda:0")
+    scene = Scene(H=8, W=8, T=256, ns=32)
+    model = GaussianParams.synthetic(2000, 3, preset="cuda", device=dev, seed=1)
+    geo = scene.geometry(dev, "cuda")
+    with torch.no_grad():
+        dense = render_volume(model, geo, make_config(model, scene, cutoff=0.0))
+        errs = []
+        for mc in (3.0, 4.0, 5.0, 6.0):
+            h = render_volume(model, geo, make_config(model, scene, cutoff=mc))
+            errs.append(((h - dense).norm() / dense.norm()).item())
+    assert errs[0] < 5e-2 and errs[1] < 3e-3 and errs[2] < 1e-4 and errs[3] < 2e-6, errs
+    assert all(errs[i + 1] <= errs[i] for i in range(3)), errs
