@@ -46,9 +46,7 @@ int set_err(int code, const char* msg) {
 constexpr int kBlock = 256;
 constexpr int kWaves = kBlock / 64;
 constexpr int kMaxK = 16;
-constexpr int kQ = 128;          // segment queue capacity per wave (drained at >= 64)
 constexpr int kNB = 64;          // Gaussians per backward workgroup
-constexpr int kFlushRounds = 8;  // forward: Gaussian rounds between round-to-nearest flushes
 constexpr float kPi = 3.14159265358979323846f;
 constexpr float kHalfLog2e = 0.72134752044448170368f;  // log2(e)/2
 
@@ -117,6 +115,32 @@ __global__ __launch_bounds__(kBlock) void preprocess_kernel(nlosgr_gaussians g, 
 }
 
 // ------------------------------------------------------------------------------------------
+// fast math (hardware v_rcp / v_sqrt / v_exp / v_log, ~1 ulp) and a polynomial atan2
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
+__device__ __forceinline__ float fsqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
+__device__ __forceinline__ float flog2(float x) { return __builtin_amdgcn_logf(x); }
+
+// atan2 with |error| < 2e-6 rad (minimax on [0,1] + octant reduction); used only for the
+// conservative footprint box, which is widened by kAngMargin.
+__device__ __forceinline__ float fast_atan2(float y, float x) {
+    const float ax = fabsf(x), ay = fabsf(y);
+    const float mx = fmaxf(ax, ay), mn = fminf(ax, ay);
+    const float a = mx > 0.f ? mn * frcp(mx) : 0.f;
+    const float s = a * a;
+    float r = fmaf(s, -0.01172120f, 0.05265332f);
+    r = fmaf(s, r, -0.11643287f);
+    r = fmaf(s, r, 0.19354346f);
+    r = fmaf(s, r, -0.33262347f);
+    r = fmaf(s, r, 0.99997726f);
+    r *= a;
+    if (ay > ax) r = 1.57079632679f - r;
+    if (x < 0.f) r = kPi - r;
+    return y < 0.f ? -r : r;
+}
+constexpr float kAngMargin = 1e-4f;
+
+// ------------------------------------------------------------------------------------------
 // per-(wall point, Gaussian) pair state
 // ------------------------------------------------------------------------------------------
 struct Pair {
@@ -169,26 +193,36 @@ __device__ __forceinline__ void pair_setup(const KArgs& k, int gi, const float m
     P.M[3] = wv1 * wv1 - kap * P.N[3];
     P.M[4] = 2.0f * (wv1 * wv2 - kap * P.N[4]);
     P.M[5] = wv2 * wv2 - kap * P.N[5];
-    // bounding-sphere cone -> (theta, phi) index box
+    // bounding-sphere cone -> (theta, phi) index box (angles via one fast atan2, widened by a margin)
     const float Rb = k.opt.cutoff * P.smax * 1.0001f + 1e-7f;
-    const float dist = sqrtf(P.q[0] * P.q[0] + P.q[1] * P.q[1] + P.q[2] * P.q[2]);
-    if (dist <= Rb) return;
-    const float sa = Rb / dist;
-    const float alpha = asinf(fminf(sa, 1.0f));
-    const float cz = fminf(fmaxf(-P.q[2] / dist, -1.0f), 1.0f);
-    const float thc = acosf(cz);
+    const float dx = -P.q[0], dy = -P.q[1], dz = -P.q[2];
+    const float rxy2 = dx * dx + dy * dy;
+    const float dist2 = rxy2 + dz * dz;
+    const float Rb2 = Rb * Rb;
+    if (dist2 <= Rb2) return;
+    const float rxy = fsqrt(rxy2);
+    const float alpha = fast_atan2(Rb, fsqrt(dist2 - Rb2)) + kAngMargin;       // asin(Rb / dist)
+    const float thc = fast_atan2(rxy, dz);                                     // acos(dz / dist)
     const float th0 = lin[0], dth = lin[1], ph0 = lin[2], dph = lin[3];
     if (dth > 0.f) {
-        P.i0 = fidx(floorf((thc - alpha - th0) / dth), 0, nt - 1);
-        P.i1 = fidx(ceilf((thc + alpha - th0) / dth), -1, nt - 1);
+        const float idth = frcp(dth);
+        P.i0 = fidx(floorf((thc - alpha - th0) * idth), 0, nt - 1);
+        P.i1 = fidx(ceilf((thc + alpha - th0) * idth), -1, nt - 1);
     }
-    if (thc - alpha > 1e-6f && thc + alpha < kPi - 1e-6f && dph > 0.f) {
-        const float phc = atan2f(-P.q[1], -P.q[0]);
-        const float dphi = asinf(fminf(sa / sinf(thc), 1.0f));
-        const float lo = phc - dphi, hi = phc + dphi;
-        if (lo > -kPi && hi < kPi) {
-            P.j0 = fidx(floorf((lo - ph0) / dph), 0, np_ - 1);
-            P.j1 = fidx(ceilf((hi - ph0) / dph), -1, np_ - 1);
+    if (thc - alpha > 1e-3f && thc + alpha < kPi - 1e-3f && dph > 0.f) {
+        // max |phi - phi_c| on the cone = asin(sin(alpha) / sin(theta_c))
+        const float sa = Rb * frcp(fsqrt(dist2));
+        const float sth = rxy * frcp(fsqrt(dist2));
+        const float ratio = sa * frcp(sth);
+        if (ratio < 0.999f) {
+            const float dphi = fast_atan2(ratio, fsqrt(1.0f - ratio * ratio)) + kAngMargin;
+            const float phc = fast_atan2(dy, dx);
+            const float lo = phc - dphi, hi = phc + dphi;
+            if (lo > -kPi && hi < kPi) {
+                const float idph = frcp(dph);
+                P.j0 = fidx(floorf((lo - ph0) * idph), 0, np_ - 1);
+                P.j1 = fidx(ceilf((hi - ph0) * idph), -1, np_ - 1);
+            }
         }
     }
 }
@@ -199,50 +233,102 @@ __device__ __forceinline__ float quadric(const float* M, float dx, float dy, flo
     return fmaf(dx, t0, fmaf(dy, t1, dz * dz * M[5]));
 }
 
-// Ray quantities: v = A d, a = |v|^2, t*, z* = u0 + t* v, m2min, in-support bin range.
+// Ray quantities: v = A d, a = |v|^2, t*, z* = u0 + t* v, m2min, in-support bin range, and
+// ks = the (fractional) bin of the closest approach.
 struct Ray {
-    float v[3], a, ts, zs[3], m2min;
+    float v[3], a, ts, zs[3], m2min, ks;
     int kl, kh;
 };
 
 template <bool DENSE>
 __device__ __forceinline__ bool ray_setup(const float* A, const float* u0, float dx, float dy, float dz, float mc2,
-                                          float r0, float dr, int nr, Ray& R) {
+                                          float r0, float inv_dr, int nr, Ray& R) {
     for (int r = 0; r < 3; ++r) R.v[r] = A[3 * r] * dx + A[3 * r + 1] * dy + A[3 * r + 2] * dz;
     R.a = R.v[0] * R.v[0] + R.v[1] * R.v[1] + R.v[2] * R.v[2];
     const float b = u0[0] * R.v[0] + u0[1] * R.v[1] + u0[2] * R.v[2];
-    R.ts = -b / R.a;
+    const float ia = frcp(R.a);
+    R.ts = -b * ia;
     for (int r = 0; r < 3; ++r) R.zs[r] = u0[r] + R.ts * R.v[r];
     R.m2min = R.zs[0] * R.zs[0] + R.zs[1] * R.zs[1] + R.zs[2] * R.zs[2];
+    R.ks = (R.ts - r0) * inv_dr;
     if (DENSE) {
         R.kl = 0; R.kh = nr - 1;
         return true;
     }
     if (!(R.m2min <= mc2)) return false;
-    const float h = sqrtf((mc2 - R.m2min) / R.a);
-    if (dr > 0.f) {
-        R.kl = fidx(ceilf((R.ts - h - r0) / dr), 0, nr);
-        R.kh = fidx(floorf((R.ts + h - r0) / dr), -1, nr - 1);
-    } else {
-        R.kl = 0; R.kh = nr - 1;
-    }
+    const float hk = fsqrt((mc2 - R.m2min) * ia) * inv_dr;
+    R.kl = fidx(ceilf(R.ks - hk), 0, nr);
+    R.kh = fidx(floorf(R.ks + hk), -1, nr - 1);
     return R.kl <= R.kh;
 }
 
 // LDS carve helper (offsets in floats, 16-byte aligned)
 __host__ __device__ __forceinline__ int al4(int n) { return (n + 3) & ~3; }
 
+constexpr int kRQ = 128;      // ray queue capacity per wave (processed in batches of 64)
+constexpr int kPD = 16;       // floats of per-pair data in LDS: A[9], u0[3], w, sigma, log2 w, rho
+
+// per-wave pair table: written by lane = pair, read by lane = ray entry
+__device__ __forceinline__ void store_pair(float* pdat, int slot, const Pair& P, float lw) {
+    float4* d = reinterpret_cast<float4*>(pdat + slot * kPD);
+    d[0] = make_float4(P.A[0], P.A[1], P.A[2], P.A[3]);
+    d[1] = make_float4(P.A[4], P.A[5], P.A[6], P.A[7]);
+    d[2] = make_float4(P.A[8], P.u0[0], P.u0[1], P.u0[2]);
+    d[3] = make_float4(P.w, P.sigma, lw, P.rho);
+}
+
+struct PairLite {
+    float A[9], u0[3], w, sigma, lw, rho;
+};
+
+__device__ __forceinline__ void load_pair(const float* pdat, int slot, PairLite& q) {
+    const float4* s = reinterpret_cast<const float4*>(pdat + slot * kPD);
+    const float4 a = s[0], b = s[1], c = s[2], d = s[3];
+    q.A[0] = a.x; q.A[1] = a.y; q.A[2] = a.z; q.A[3] = a.w;
+    q.A[4] = b.x; q.A[5] = b.y; q.A[6] = b.z; q.A[7] = b.w;
+    q.A[8] = c.x; q.u0[0] = c.y; q.u0[1] = c.z; q.u0[2] = c.w;
+    q.w = d.x; q.sigma = d.y; q.lw = d.z; q.rho = d.w;
+}
+
+__device__ __forceinline__ unsigned pack_ray(int slot, int i, int j) {
+    return (unsigned)slot | ((unsigned)i << 8) | ((unsigned)j << 20);
+}
+
+// Candidate enumeration (lane = pair): quadric test only; passing (pair, ray) go to the ray queue.
+// Returns when the queue holds >= 64 entries or every lane has exhausted its box.
+template <bool DENSE>
+__device__ __forceinline__ void enumerate(const Pair& P, bool& more, int& ci, int& cj, const float2* tth,
+                                          const float2* tph, unsigned* rayq, int& cnt) {
+    const int lane = lane_id();
+    while (__builtin_amdgcn_ballot_w64(more)) {
+        bool pass = false;
+        unsigned e = 0;
+        if (more) {
+            const float2 th = tth[ci], ph = tph[cj];
+            if (DENSE || quadric(P.M, th.x * ph.x, th.x * ph.y, th.y) >= 0.f) {
+                pass = true;
+                e = pack_ray(lane, ci, cj);
+            }
+            if (++cj > P.j1) { cj = P.j0; ++ci; }
+            more = ci <= P.i1;
+        }
+        const unsigned long long m = __builtin_amdgcn_ballot_w64(pass);
+        if (pass) rayq[cnt + lanes_below(m)] = e;
+        cnt += __popcll(m);
+        if (cnt >= 64) return;
+    }
+}
+
 struct FwdLayout {
-    int acc, tot, queue, qx, qray, wave_stride, total;
+    int acc0, acc1, pdat, rayq, wave_stride, total;
     __host__ __device__ FwdLayout(int nr, int nt, int np_) {
         const int off = al4(2 * (nt + np_));  // float2 theta table [nt], float2 phi table [np]
-        acc = 0;                              // [nr + 64] window target (+64: windows overrun nr)
-        tot = al4(nr + 64);                   // [nr] round-to-nearest totals
-        queue = tot + al4(nr);                // float4 [kQ] (alpha, gamma, lam_s, kl|len)
-        qx = queue + 4 * kQ;                  // float4 [kQ] (sin theta, sigma c dT, w c dT, ray)
-        qray = qx + 4 * kQ;
-        wave_stride = al4(qray);
-        acc += off; tot += off; queue += off; qx += off;
+        acc0 = 0;                             // two wave-private histograms (alternating segments)
+        acc1 = al4(nr + 64);
+        pdat = acc1 + al4(nr + 64);           // [64][kPD]
+        rayq = pdat + 64 * kPD;               // uint [kRQ]
+        wave_stride = al4(rayq + kRQ);
+        acc0 += off; acc1 += off; pdat += off; rayq += off;
         total = off + kWaves * wave_stride;
     }
 };
@@ -250,39 +336,102 @@ struct FwdLayout {
 // ------------------------------------------------------------------------------------------
 // forward
 // ------------------------------------------------------------------------------------------
-template <int MODE, bool RAYS>
-__device__ __forceinline__ void fwd_drain(float* acc, const float4* queue, const float4* qx, int cnt, float* rout,
-                                          int nr, float rscale, float f0log2) {
+// Segment record of one (pair, ray): value(lam) = exp2(al + ga (lam - ls)^2) at bin kl + lam,
+// lam in [0, len); histogram weight st = sin(theta_i).
+struct Seg {
+    float al, ga, ls, st, sc, wc;  // sc = sigma c dT, wc = w c dT (netf)
+    int kl, len, ray;
+};
+
+__device__ __forceinline__ Seg readlane_seg(const Seg& s, int l) {
+    Seg r;
+    r.al = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(s.al), l));
+    r.ga = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(s.ga), l));
+    r.ls = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(s.ls), l));
+    r.st = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(s.st), l));
+    r.sc = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(s.sc), l));
+    r.wc = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(s.wc), l));
+    r.kl = __builtin_amdgcn_readlane(s.kl, l);
+    r.len = __builtin_amdgcn_readlane(s.len, l);
+    r.ray = __builtin_amdgcn_readlane(s.ray, l);
+    return r;
+}
+
+// lane = ray-queue entry: exact support test + segment record; then the wave walks the passing
+// segments (2 at a time, alternating histogram copies so two read-add-writes are in flight) with
+// lane = bin.  Plain LDS read/add/write: each instruction touches 64 distinct addresses of a
+// wave-private histogram, so it is race-free and rounds to nearest.
+template <int MODE, bool DENSE, bool RAYS>
+__device__ __forceinline__ void fwd_rays(const unsigned* rayq, int cnt, const float* pdat, const float2* tth,
+                                         const float2* tph, float* acc0, float* acc1, float* rout, int np_, int nr,
+                                         float mc2, float r0, float dr, float inv_dr, float rscale, float f0log2) {
     const int lane = lane_id();
-    for (int s = 0; s < cnt; ++s) {
-        const float4 rec = queue[s];
-        const float4 ex = qx[s];
-        const unsigned bits = __float_as_uint(rec.w);
-        const int kl = bits & 0xFFFF, len = bits >> 16;
-        float* dst = acc + kl;
-        float* rrow = RAYS ? rout + (size_t)__float_as_int(ex.w) * nr + kl : nullptr;
-        if (MODE == NLOSGR_MODE_NOOCL) {
-            // value = w pdf = exp2(alpha + gamma (lam - lam_s)^2); histogram adds sin(theta) x value
-            for (int m0 = 0; m0 < len; m0 += 64) {
-                const int lam = m0 + lane;
-                if (lam < len) {
-                    const float t = (float)lam - rec.z;
-                    const float val = fast_exp2(fmaf(rec.y, t * t, rec.x));
-                    atomicAdd(dst + lam, ex.x * val);
-                    if (RAYS) atomicAdd(rrow + lam, rscale * val);
+    Seg sg;
+    bool pass = false;
+    if (lane < cnt) {
+        const unsigned e = rayq[lane];
+        const int slot = e & 0xFF, i = (e >> 8) & 0xFFF, j = e >> 20;
+        PairLite q;
+        load_pair(pdat, slot, q);
+        const float2 th = tth[i], ph = tph[j];
+        Ray R;
+        if (ray_setup<DENSE>(q.A, q.u0, th.x * ph.x, th.x * ph.y, th.y, mc2, r0, inv_dr, nr, R)) {
+            pass = true;
+            sg.al = fmaf(-kHalfLog2e, R.m2min, MODE == NLOSGR_MODE_NOOCL ? q.lw : 0.f);
+            sg.ga = -kHalfLog2e * R.a * dr * dr;
+            sg.ls = R.ks - (float)R.kl;
+            sg.st = th.x;
+            sg.sc = q.sigma;
+            sg.wc = q.w;
+            sg.kl = R.kl;
+            sg.len = R.kh - R.kl + 1;
+            sg.ray = i * np_ + j;
+        }
+    }
+    unsigned long long mask = __builtin_amdgcn_ballot_w64(pass);
+    if (MODE == NLOSGR_MODE_NOOCL) {
+        while (mask) {
+            const int l0 = __builtin_ctzll(mask);
+            mask &= mask - 1;
+            const bool two = mask != 0;
+            const int l1 = two ? __builtin_ctzll(mask) : l0;
+            if (two) mask &= mask - 1;
+            const Seg a = readlane_seg(sg, l0);
+            const Seg b = readlane_seg(sg, l1);
+            const int lenb = two ? b.len : 0;
+            const int lmax = max(a.len, lenb);
+            float* pa = acc0 + a.kl;
+            float* pb = acc1 + b.kl;
+            float ta = (float)lane - a.ls, tb = (float)lane - b.ls;
+            for (int lam = lane, m0 = 0; m0 < lmax; m0 += 64, lam += 64, ta += 64.f, tb += 64.f) {
+                const bool ia = lam < a.len, ib = lam < lenb;
+                const float va = ia ? fast_exp2(fmaf(a.ga, ta * ta, a.al)) : 0.f;
+                const float vb = ib ? fast_exp2(fmaf(b.ga, tb * tb, b.al)) : 0.f;
+                const float xa = ia ? pa[lam] : 0.f;
+                const float xb = ib ? pb[lam] : 0.f;
+                if (ia) pa[lam] = fmaf(a.st, va, xa);
+                if (ib) pb[lam] = fmaf(b.st, vb, xb);
+                if (RAYS) {
+                    if (ia) atomicAdd(rout + (size_t)a.ray * nr + a.kl + lam, rscale * va);
+                    if (ib) atomicAdd(rout + (size_t)b.ray * nr + b.kl + lam, rscale * vb);
                 }
             }
-        } else {
-            // netf: T_k = prod_{k'<k} (exp(-sigma pdf c dT) + 1e-7) front-to-back along the ray
-            // (gaussian_model.py:317-321), an exclusive log-domain prefix scan across the window's
-            // lanes with the carry kept between windows; value = w c dT pdf T.
-            float logT = (float)kl * f0log2;
-            for (int m0 = 0; m0 < len; m0 += 64) {
-                const int lam = m0 + lane;
-                const bool in = lam < len;
-                const float t = (float)lam - rec.z;
-                const float pdf = in ? fast_exp2(fmaf(rec.y, t * t, rec.x)) : 0.f;
-                const float lf = in ? __log2f(__expf(-ex.y * pdf) + 1e-7f) : 0.f;
+        }
+    } else {
+        // netf: T_k = prod_{k'<k} (exp(-sigma pdf c dT) + 1e-7) front-to-back along the ray
+        // (gaussian_model.py:317-321) as an exclusive log-domain prefix scan across the 64 lanes of
+        // each window, carried between windows; value = w c dT pdf T.
+        while (mask) {
+            const int l0 = __builtin_ctzll(mask);
+            mask &= mask - 1;
+            const Seg a = readlane_seg(sg, l0);
+            float* pa = acc0 + a.kl;
+            float logT = (float)a.kl * f0log2;
+            float ta = (float)lane - a.ls;
+            for (int lam = lane, m0 = 0; m0 < a.len; m0 += 64, lam += 64, ta += 64.f) {
+                const bool in = lam < a.len;
+                const float pdf = in ? fast_exp2(fmaf(a.ga, ta * ta, a.al)) : 0.f;
+                const float lf = in ? flog2(__expf(-a.sc * pdf) + 1e-7f) : 0.f;
                 float incl = lf;
 #pragma unroll
                 for (int o = 1; o < 64; o <<= 1) {
@@ -290,9 +439,9 @@ __device__ __forceinline__ void fwd_drain(float* acc, const float4* queue, const
                     if (lane >= o) incl += u;
                 }
                 if (in) {
-                    const float val = ex.z * pdf * fast_exp2(logT + (incl - lf));
-                    atomicAdd(dst + lam, ex.x * val);
-                    if (RAYS) atomicAdd(rrow + lam, rscale * val);
+                    const float val = a.wc * pdf * fast_exp2(logT + (incl - lf));
+                    pa[lam] += a.st * val;
+                    if (RAYS) atomicAdd(rout + (size_t)a.ray * nr + a.kl + lam, rscale * val);
                 }
                 logT += __shfl(incl, 63);
             }
@@ -309,18 +458,20 @@ __global__ __launch_bounds__(kBlock) void fwd_kernel(KArgs k) {
     float2* tph = tth + nt;
     const int wave = threadIdx.x >> 6, lane = lane_id();
     float* wb = smem + wave * L.wave_stride;
-    float* acc = wb + L.acc;
-    float* tot = wb + L.tot;
-    float4* queue = reinterpret_cast<float4*>(wb + L.queue);
-    float4* qx = reinterpret_cast<float4*>(wb + L.qx);
+    float* acc0 = wb + L.acc0;
+    float* acc1 = wb + L.acc1;
+    float* pdat = wb + L.pdat;
+    unsigned* rayq = reinterpret_cast<unsigned*>(wb + L.rayq);
     const int p = blockIdx.x;
 
     for (int t = threadIdx.x; t < nt; t += blockDim.x)
         tth[t] = make_float2(k.geo.sin_theta[(size_t)p * nt + t], k.geo.cos_theta[(size_t)p * nt + t]);
     for (int t = threadIdx.x; t < np_; t += blockDim.x)
         tph[t] = make_float2(k.geo.cos_phi[(size_t)p * np_ + t], k.geo.sin_phi[(size_t)p * np_ + t]);
-    for (int t = lane; t < nr + 64; t += 64) acc[t] = 0.f;
-    for (int t = lane; t < nr; t += 64) tot[t] = 0.f;
+    for (int t = lane; t < nr + 64; t += 64) {
+        acc0[t] = 0.f;
+        acc1[t] = 0.f;
+    }
     __syncthreads();
 
     const float px = k.geo.wall[3 * p], py = k.geo.wall[3 * p + 1], pz = k.geo.wall[3 * p + 2];
@@ -334,9 +485,7 @@ __global__ __launch_bounds__(kBlock) void fwd_kernel(KArgs k) {
     float* rout = RAYS ? k.ray_out + (size_t)p * nt * np_ * nr : nullptr;
     const float rscale = k.opt.ray_scale;
 
-    int cnt = 0;
-    int round = 0;
-    for (int base = wave * 64; base < k.g.ng; base += kBlock, ++round) {
+    for (int base = wave * 64; base < k.g.ng; base += kBlock) {
         const int gi = base + lane;
         Pair P;
         float mu[3];
@@ -346,65 +495,36 @@ __global__ __launch_bounds__(kBlock) void fwd_kernel(KArgs k) {
             load_rec(k.recs[gi], P, mu);
             pair_setup<PRESET, DENSE>(k, gi, mu, px, py, pz, lin, mc2, P);
             more = (P.w > 0.f) && P.i0 <= P.i1 && P.j0 <= P.j1;
+            // netf keeps w, sigma scaled by c dT in the pair table
+            if (MODE == NLOSGR_MODE_NETF) { P.w *= cdt; P.sigma *= cdt; }
+            store_pair(pdat, lane, P, more ? flog2(P.w) : 0.f);
+            if (MODE == NLOSGR_MODE_NETF) { P.w /= cdt; P.sigma /= cdt; }
         }
-        int ci = P.i0, cj = P.j0;
-        const float lw = (MODE == NLOSGR_MODE_NOOCL && more) ? __log2f(P.w) : 0.f;
-        while (__builtin_amdgcn_ballot_w64(more)) {
-            bool pass = false;
-            float4 rec, ex;
-            if (more) {
-                const float2 th = tth[ci], ph = tph[cj];
-                const float dx = th.x * ph.x, dy = th.x * ph.y, dz = th.y;
-                if (DENSE || quadric(P.M, dx, dy, dz) >= 0.f) {
-                    Ray R;
-                    if (ray_setup<DENSE>(P.A, P.u0, dx, dy, dz, mc2, r0, dr, nr, R)) {
-                        // window coordinates lam = k - kl; log2(value) = alpha + gamma (lam - lam_s)^2
-                        rec = make_float4(lw - kHalfLog2e * R.m2min, -kHalfLog2e * R.a * dr * dr,
-                                          (R.ts - r0) * inv_dr - (float)R.kl,
-                                          __uint_as_float((unsigned)R.kl | ((unsigned)(R.kh - R.kl + 1) << 16)));
-                        ex = make_float4(th.x, P.sigma * cdt, P.w * cdt, __int_as_float(ci * np_ + cj));
-                        pass = true;
-                    }
-                }
-                if (++cj > P.j1) { cj = P.j0; ++ci; }
-                more = ci <= P.i1;
-            }
-            const unsigned long long m = __builtin_amdgcn_ballot_w64(pass);
-            if (pass) {
-                const int pos = cnt + lanes_below(m);
-                queue[pos] = rec;
-                qx[pos] = ex;
-            }
-            cnt += __popcll(m);
-            if (cnt >= 64) {
-                wave_sync();
-                fwd_drain<MODE, RAYS>(acc, queue, qx, cnt, rout, nr, rscale, f0log2);
-                wave_sync();
-                cnt = 0;
-            }
+        wave_sync();
+        int ci = P.i0, cj = P.j0, cnt = 0;
+        while (true) {
+            enumerate<DENSE>(P, more, ci, cj, tth, tph, rayq, cnt);
+            if (cnt == 0) break;
+            wave_sync();
+            const int nb = min(cnt, 64);
+            fwd_rays<MODE, DENSE, RAYS>(rayq, nb, pdat, tth, tph, acc0, acc1, rout, np_, nr, mc2, r0, dr, inv_dr,
+                                        rscale, f0log2);
+            wave_sync();
+            if (lane < cnt - nb) rayq[lane] = rayq[nb + lane];
+            wave_sync();
+            cnt -= nb;
         }
-        if ((round + 1) % kFlushRounds == 0) {
-            wave_sync();
-            fwd_drain<MODE, RAYS>(acc, queue, qx, cnt, rout, nr, rscale, f0log2);
-            cnt = 0;
-            wave_sync();
-            for (int t = lane; t < nr; t += 64) {
-                tot[t] += acc[t];
-                acc[t] = 0.f;
-            }
-            wave_sync();
-        }
+        wave_sync();
     }
-    wave_sync();
-    fwd_drain<MODE, RAYS>(acc, queue, qx, cnt, rout, nr, rscale, f0log2);
-    wave_sync();
-    for (int t = lane; t < nr; t += 64) tot[t] += acc[t];
     __syncthreads();
     if (k.hist_out) {
         const float hs = k.geo.hscale[p];
         for (int t = threadIdx.x; t < nr; t += blockDim.x) {
             float s = 0.f;
-            for (int w = 0; w < kWaves; ++w) s += smem[w * L.wave_stride + L.tot + t];
+            for (int w = 0; w < kWaves; ++w) {
+                const float* b = smem + w * L.wave_stride;
+                s += b[L.acc0 + t] + b[L.acc1 + t];
+            }
             k.hist_out[(size_t)p * nr + t] = s * k.geo.att[t] * hs;
         }
     }
@@ -413,19 +533,22 @@ __global__ __launch_bounds__(kBlock) void fwd_kernel(KArgs k) {
 // ------------------------------------------------------------------------------------------
 // backward
 // ------------------------------------------------------------------------------------------
+constexpr int kChunk = 32;   // segments are split into chunks of <= kChunk bins (lane-serial work)
+
 struct BwdLayout {
-    int recs, wave_base, wave_stride, grow, tth, tph, pd, prho, pacc, queue, red, total;
+    int recs, wave_base, wave_stride, grow, tth, tph, pdat, pacc, rows, rayq, chq, red, total;
     __host__ __device__ BwdLayout(int nr, int nt, int np_) {
         recs = 0;                            // GaussRec [kNB] (20 floats each)
         wave_base = al4(kNB * 20);
         grow = 0;                            // [nr] upstream gradient row x att x hscale
         tth = al4(nr);                       // float2 [nt]
         tph = tth + al4(2 * nt);             // float2 [np]
-        pd = tph + al4(2 * np_);             // float4 [64] (u0, w)
-        prho = pd + 4 * 64;                  // [64] rho
-        pacc = prho + 64;                    // [64][16] per-pair accumulators
-        queue = pacc + 16 * 64;              // uint2 [kQ]
-        wave_stride = al4(queue + 2 * kQ);
+        pdat = tph + al4(2 * np_);           // [64][kPD] pair table
+        pacc = pdat + 64 * kPD;              // [64][16] per-pair accumulators
+        rows = pacc + 64 * 16;               // [64][16] per-chunk results (reduction staging)
+        rayq = rows + 64 * 16;               // uint [kRQ]
+        chq = rayq + kRQ;                    // uint2 [kRQ] chunk queue
+        wave_stride = al4(chq + 2 * kRQ);
         red = wave_base;                     // final reduction reuses the wave regions
         total = wave_base + kWaves * wave_stride;
         const int need_red = wave_base + kWaves * 64 * 29;
@@ -433,93 +556,174 @@ struct BwdLayout {
     }
 };
 
+// lane = chunk (<= kChunk bins of one ray) run serially; results (linear in the chunk's sums) are
+// grouped by pair with a ballot match and added to the pair accumulators by one leader per pair.
 template <int MODE, bool RAYS>
-__device__ __forceinline__ void bwd_drain(const GaussRec* srec, const float* grow, const float2* tth,
-                                          const float2* tph, const float4* pd, const float* prho, float* pacc,
-                                          const uint2* queue, int cnt, const float* gray, int np_, float r0, float dr,
-                                          int nr, float cdt, float f0log2, float rscale) {
+__device__ __forceinline__ void bwd_chunks(const uint2* chq, int cnt, const float* pdat, const float* grow,
+                                           const float2* tth, const float2* tph, float* pacc, float* rows,
+                                           const float* gray, int np_, int nr, float r0, float dr, float inv_dr,
+                                           float cdt, float f0log2, float rscale) {
     const int lane = lane_id();
-    if (lane >= cnt) return;
-    const uint2 e = queue[lane];
-    const int slot = e.x & 0xFF, i = (e.x >> 8) & 0xFFF, j = e.x >> 20;
-    const int kl = e.y & 0xFFFF, kh = e.y >> 16;
-    const float4 pdat = pd[slot];
-    const float u0[3] = {pdat.x, pdat.y, pdat.z};
-    const float w = pdat.w;
-    const GaussRec rr = srec[slot];
-    const float A[9] = {rr.b.x, rr.b.y, rr.b.z, rr.b.w, rr.c.x, rr.c.y, rr.c.z, rr.c.w, rr.d.x};
-    const float sigma = rr.a.w;
-    const float rho = prho[slot];
-    const float2 th = tth[i], ph = tph[j];
-    const float dx = th.x * ph.x, dy = th.x * ph.y, dz = th.y;
-    Ray R;
-    ray_setup<true>(A, u0, dx, dy, dz, 0.f, r0, dr, nr, R);
-    const float sti = th.x;
-    const float* grw = RAYS && gray ? gray + (size_t)(i * np_ + j) * nr : nullptr;
-    float S0 = 0.f, S1 = 0.f, S2 = 0.f, dsig = 0.f, drho = 0.f;  // S_n = sum_k (dL/dpdf_k) pdf_k dl^n
-    if (MODE == NLOSGR_MODE_NOOCL) {
-        float Hs = 0.f;
-        for (int kk = kl; kk <= kh; ++kk) {
-            const float dl = fmaf((float)kk, dr, r0) - R.ts;
-            const float pdf = fast_exp2(-kHalfLog2e * fmaf(R.a * dl, dl, R.m2min));
-            float H = grow[kk] * sti;
-            if (RAYS && grw) H += grw[kk] * rscale;
-            const float hp = H * pdf;
-            Hs += hp;
-            const float t1 = hp * dl;
-            S0 += hp; S1 += t1; S2 = fmaf(t1, dl, S2);
+    const bool act = lane < cnt;
+    int slot = 64 + lane;   // inactive lanes get unique dummy keys
+    if (act) {
+        const uint2 e = chq[lane];
+        slot = e.x & 0xFF;
+        const int i = (e.x >> 8) & 0xFFF, j = e.x >> 20;
+        const int kl = e.y & 0xFFFF, kh = e.y >> 16;
+        PairLite q;
+        load_pair(pdat, slot, q);
+        const float2 th = tth[i], ph = tph[j];
+        const float dx = th.x * ph.x, dy = th.x * ph.y, dz = th.y;
+        Ray R;
+        ray_setup<true>(q.A, q.u0, dx, dy, dz, 0.f, r0, inv_dr, nr, R);
+        const float sti = th.x;
+        const float* grw = RAYS && gray ? gray + (size_t)(i * np_ + j) * nr : nullptr;
+        // centred bin coordinate kap = k - ks: pdf = exp2(c0 + c2 kap^2), dl = kap dr
+        const float c0 = -kHalfLog2e * R.m2min;
+        const float c2 = -kHalfLog2e * R.a * dr * dr;
+        float S0 = 0.f, S1 = 0.f, S2 = 0.f, dsig = 0.f, drho = 0.f;  // S_n = sum (dL/dpdf) pdf kap^n
+        if (MODE == NLOSGR_MODE_NOOCL) {
+            float kap = (float)kl - R.ks;
+            const bool rg = RAYS && grw;
+            for (int kk = kl; kk <= kh; ++kk, kap += 1.0f) {
+                const float pdf = fast_exp2(fmaf(c2, kap * kap, c0));
+                const float H = rg ? fmaf(grow[kk], sti, grw[kk] * rscale) : grow[kk];
+                const float hp = H * pdf;
+                const float t1 = hp * kap;
+                S0 += hp; S1 += t1; S2 = fmaf(t1, kap, S2);
+            }
+            if (!rg) { S0 *= sti; S1 *= sti; S2 *= sti; }
+            dsig = S0 * q.rho;
+            drho = S0 * q.sigma;
+            S0 *= q.w; S1 *= q.w; S2 *= q.w;
+        } else {
+            // netf (whole ray per chunk): dL/dD_j = c rho H_j T_j + (sum_{k>j} H_k out_k) f'_j / f_j
+            const float T0 = fast_exp2((float)kl * f0log2);
+            float T = T0, Etot = 0.f;
+            float kap = (float)kl - R.ks;
+            for (int kk = kl; kk <= kh; ++kk, kap += 1.0f) {
+                const float pdf = fast_exp2(fmaf(c2, kap * kap, c0));
+                const float D = q.sigma * pdf;
+                float H = grow[kk] * sti;
+                if (RAYS && grw) H += grw[kk] * rscale;
+                Etot += H * cdt * q.rho * D * T;
+                T *= (__expf(-D * cdt) + 1e-7f);
+            }
+            T = T0;
+            float pre = 0.f;
+            kap = (float)kl - R.ks;
+            for (int kk = kl; kk <= kh; ++kk, kap += 1.0f) {
+                const float pdf = fast_exp2(fmaf(c2, kap * kap, c0));
+                const float D = q.sigma * pdf;
+                float H = grow[kk] * sti;
+                if (RAYS && grw) H += grw[kk] * rscale;
+                const float ee = __expf(-D * cdt);
+                const float f = ee + 1e-7f;
+                pre += H * cdt * q.rho * D * T;
+                const float dD = cdt * q.rho * H * T + (Etot - pre) * (-cdt * ee) * frcp(f);
+                drho += H * cdt * D * T;
+                dsig += dD * pdf;
+                const float hp = dD * q.sigma * pdf;
+                const float t1 = hp * kap;
+                S0 += hp; S1 += t1; S2 = fmaf(t1, kap, S2);
+                T *= f;
+            }
         }
-        dsig = Hs * rho;
-        drho = Hs * sigma;
-        S0 *= w; S1 *= w; S2 *= w;
-    } else {
-        // netf: dL/dD_j = c rho H_j T_j + (sum_{k>j} H_k out_k) f'_j / f_j, two forward passes
-        const float T0 = fast_exp2((float)kl * f0log2);
-        float T = T0, Etot = 0.f;
-        for (int kk = kl; kk <= kh; ++kk) {
-            const float dl = fmaf((float)kk, dr, r0) - R.ts;
-            const float pdf = fast_exp2(-kHalfLog2e * fmaf(R.a * dl, dl, R.m2min));
-            const float D = sigma * pdf;
-            float H = grow[kk] * sti;
-            if (RAYS && grw) H += grw[kk] * rscale;
-            Etot += H * cdt * rho * D * T;
-            T *= (__expf(-D * cdt) + 1e-7f);
+        S1 *= dr;
+        S2 *= dr * dr;
+        // pdf = exp(-|z|^2/2), z = z* + dl v  ->  dL/du0 = -sum P z,  dL/dv = -sum P r z,  dA += dV (x) d
+        float zv[3], dV[3];
+        for (int r = 0; r < 3; ++r) {
+            zv[r] = S0 * R.zs[r] + S1 * R.v[r];
+            dV[r] = -(R.ts * zv[r] + S1 * R.zs[r] + S2 * R.v[r]);
         }
-        T = T0;
-        float pre = 0.f;
-        for (int kk = kl; kk <= kh; ++kk) {
-            const float dl = fmaf((float)kk, dr, r0) - R.ts;
-            const float pdf = fast_exp2(-kHalfLog2e * fmaf(R.a * dl, dl, R.m2min));
-            const float D = sigma * pdf;
-            float H = grow[kk] * sti;
-            if (RAYS && grw) H += grw[kk] * rscale;
-            const float ee = __expf(-D * cdt);
-            const float f = ee + 1e-7f;
-            pre += H * cdt * rho * D * T;
-            const float dD = cdt * rho * H * T + (Etot - pre) * (-cdt * ee) / f;
-            drho += H * cdt * D * T;
-            dsig += dD * pdf;
-            const float hp = dD * sigma * pdf;
-            const float t1 = hp * dl;
-            S0 += hp; S1 += t1; S2 = fmaf(t1, dl, S2);
-            T *= f;
+        float4* row = reinterpret_cast<float4*>(rows + lane * 16);
+        row[0] = make_float4(-zv[0], -zv[1], -zv[2], dV[0] * dx);
+        row[1] = make_float4(dV[0] * dy, dV[0] * dz, dV[1] * dx, dV[1] * dy);
+        row[2] = make_float4(dV[1] * dz, dV[2] * dx, dV[2] * dy, dV[2] * dz);
+        row[3] = make_float4(dsig, drho, 0.f, 0.f);
+    }
+    // group lanes by pair slot (7-bit keys) and let the lowest lane of each group reduce it
+    unsigned long long peers = ~0ull;
+#pragma unroll
+    for (int b = 0; b < 7; ++b) {
+        const bool bit = (slot >> b) & 1;
+        const unsigned long long m = __builtin_amdgcn_ballot_w64(bit);
+        peers &= bit ? m : ~m;
+    }
+    wave_sync();
+    const bool leader = act && (lanes_below(peers) == 0);
+    if (leader) {
+        float s[16];
+#pragma unroll
+        for (int t = 0; t < 16; ++t) s[t] = 0.f;
+        unsigned long long pm = peers;
+        while (pm) {
+            const int l = __builtin_ctzll(pm);
+            pm &= pm - 1;
+            const float4* row = reinterpret_cast<const float4*>(rows + l * 16);
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const float4 v = row[t];
+                s[4 * t] += v.x; s[4 * t + 1] += v.y; s[4 * t + 2] += v.z; s[4 * t + 3] += v.w;
+            }
+        }
+        float4* pa = reinterpret_cast<float4*>(pacc + slot * 16);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            float4 v = pa[t];
+            v.x += s[4 * t]; v.y += s[4 * t + 1]; v.z += s[4 * t + 2]; v.w += s[4 * t + 3];
+            pa[t] = v;
         }
     }
-    // pdf = exp(-|z|^2/2), z = z* + dl v  ->  dL/du0 = -sum P z,  dL/dv = -sum P r z
-    float* pa = pacc + slot * 16;
-    float zv[3], dV[3];
-    for (int r = 0; r < 3; ++r) {
-        zv[r] = S0 * R.zs[r] + S1 * R.v[r];
-        dV[r] = -(R.ts * zv[r] + S1 * R.zs[r] + S2 * R.v[r]);
-        atomicAdd(pa + r, -zv[r]);
+    wave_sync();
+}
+
+// lane = ray-queue entry: exact support test, then its chunks are appended to the chunk queue
+// (drained 64 at a time).
+template <int MODE, bool DENSE, bool RAYS>
+__device__ __forceinline__ void bwd_rays(const unsigned* rayq, int cnt, uint2* chq, int& ccnt, const float* pdat,
+                                         const float* grow, const float2* tth, const float2* tph, float* pacc,
+                                         float* rows, const float* gray, int np_, int nr, float mc2, float r0,
+                                         float dr, float inv_dr, float cdt, float f0log2, float rscale) {
+    const int lane = lane_id();
+    int ckl = 1, ckh = 0, step = 1;
+    unsigned cid = 0;
+    if (lane < cnt) {
+        cid = rayq[lane];
+        const int slot = cid & 0xFF, i = (cid >> 8) & 0xFFF, j = cid >> 20;
+        PairLite q;
+        load_pair(pdat, slot, q);
+        const float2 th = tth[i], ph = tph[j];
+        Ray R;
+        if (ray_setup<DENSE>(q.A, q.u0, th.x * ph.x, th.x * ph.y, th.y, mc2, r0, inv_dr, nr, R)) {
+            ckl = R.kl; ckh = R.kh;
+            const int len = R.kh - R.kl + 1;
+            const int nch = (len + kChunk - 1) / kChunk;
+            step = MODE == NLOSGR_MODE_NETF ? len : (len + nch - 1) / nch;
+        }
     }
-    for (int r = 0; r < 3; ++r) {  // dA += dV (x) d
-        atomicAdd(pa + 3 + 3 * r, dV[r] * dx);
-        atomicAdd(pa + 4 + 3 * r, dV[r] * dy);
-        atomicAdd(pa + 5 + 3 * r, dV[r] * dz);
+    while (__builtin_amdgcn_ballot_w64(ckl <= ckh)) {
+        const bool pass = ckl <= ckh;
+        uint2 e;
+        if (pass) {
+            const int ce = min(ckh, ckl + step - 1);
+            e = make_uint2(cid, (unsigned)ckl | ((unsigned)ce << 16));
+            ckl = ce + 1;
+        }
+        const unsigned long long m = __builtin_amdgcn_ballot_w64(pass);
+        if (pass) chq[ccnt + lanes_below(m)] = e;
+        ccnt += __popcll(m);
+        if (ccnt >= 64) {
+            wave_sync();
+            bwd_chunks<MODE, RAYS>(chq, 64, pdat, grow, tth, tph, pacc, rows, gray, np_, nr, r0, dr, inv_dr, cdt,
+                                   f0log2, rscale);
+            if (lane < ccnt - 64) chq[lane] = chq[64 + lane];
+            wave_sync();
+            ccnt -= 64;
+        }
     }
-    atomicAdd(pa + 12, dsig);
-    atomicAdd(pa + 13, drho);
 }
 
 template <int PRESET, int MODE, bool DENSE, bool RAYS>
@@ -533,10 +737,11 @@ __global__ __launch_bounds__(kBlock) void bwd_kernel(KArgs k) {
     float* grow = wb + L.grow;
     float2* tth = reinterpret_cast<float2*>(wb + L.tth);
     float2* tph = reinterpret_cast<float2*>(wb + L.tph);
-    float4* pd = reinterpret_cast<float4*>(wb + L.pd);
-    float* prho = wb + L.prho;
+    float* pdat = wb + L.pdat;
     float* pacc = wb + L.pacc;
-    uint2* queue = reinterpret_cast<uint2*>(wb + L.queue);
+    float* rows = wb + L.rows;
+    unsigned* rayq = reinterpret_cast<unsigned*>(wb + L.rayq);
+    uint2* chq = reinterpret_cast<uint2*>(wb + L.chq);
 
     const int gb = blockIdx.x * kNB;
     const int gi = gb + lane;
@@ -554,6 +759,7 @@ __global__ __launch_bounds__(kBlock) void bwd_kernel(KArgs k) {
     const float mc2 = k.opt.cutoff * k.opt.cutoff;
     const float r0 = k.geo.r[0];
     const float dr = nr > 1 ? (k.geo.r[nr - 1] - r0) / (float)(nr - 1) : 0.f;
+    const float inv_dr = dr > 0.f ? 1.0f / dr : 0.f;
     const float cdt = k.opt.c_deltaT;
     const float f0log2 = log2f(1.0f + 1e-7f);
     const float rscale = k.opt.ray_scale;
@@ -585,46 +791,28 @@ __global__ __launch_bounds__(kBlock) void bwd_kernel(KArgs k) {
         if (active) {
             pair_setup<PRESET, DENSE>(k, gi, mu, px, py, pz, k.geo.grid_lin + 4 * (size_t)p, mc2, P);
             more = (P.w > 0.f) && P.i0 <= P.i1 && P.j0 <= P.j1;
-            pd[lane] = make_float4(P.u0[0], P.u0[1], P.u0[2], P.w);
-            prho[lane] = P.rho;
+            store_pair(pdat, lane, P, 0.f);
         }
         const float* gray = RAYS && k.grad_ray ? k.grad_ray + (size_t)p * nt * np_ * nr : nullptr;
         wave_sync();
-        int ci = P.i0, cj = P.j0;
-        int cnt = 0;
-        while (__builtin_amdgcn_ballot_w64(more)) {
-            bool pass = false;
-            uint2 e;
-            if (more) {
-                const float2 th = tth[ci], ph = tph[cj];
-                const float dx = th.x * ph.x, dy = th.x * ph.y, dz = th.y;
-                if (DENSE || quadric(P.M, dx, dy, dz) >= 0.f) {
-                    Ray R;
-                    if (ray_setup<DENSE>(P.A, P.u0, dx, dy, dz, mc2, r0, dr, nr, R)) {
-                        e = make_uint2((unsigned)lane | ((unsigned)ci << 8) | ((unsigned)cj << 20),
-                                       (unsigned)R.kl | ((unsigned)R.kh << 16));
-                        pass = true;
-                    }
-                }
-                if (++cj > P.j1) { cj = P.j0; ++ci; }
-                more = ci <= P.i1;
-            }
-            const unsigned long long m = __builtin_amdgcn_ballot_w64(pass);
-            if (pass) queue[cnt + lanes_below(m)] = e;
-            cnt += __popcll(m);
-            if (cnt >= 64) {
-                wave_sync();
-                bwd_drain<MODE, RAYS>(srec, grow, tth, tph, pd, prho, pacc, queue, 64, gray, np_, r0, dr, nr, cdt,
-                                      f0log2, rscale);
-                wave_sync();
-                if (lane < cnt - 64) queue[lane] = queue[64 + lane];
-                wave_sync();
-                cnt -= 64;
-            }
+        int ci = P.i0, cj = P.j0, cnt = 0, ccnt = 0;
+        while (true) {
+            enumerate<DENSE>(P, more, ci, cj, tth, tph, rayq, cnt);
+            if (cnt == 0) break;
+            wave_sync();
+            const int nb = min(cnt, 64);
+            bwd_rays<MODE, DENSE, RAYS>(rayq, nb, chq, ccnt, pdat, grow, tth, tph, pacc, rows, gray, np_, nr, mc2, r0,
+                                        dr, inv_dr, cdt, f0log2, rscale);
+            wave_sync();
+            if (lane < cnt - nb) rayq[lane] = rayq[nb + lane];
+            wave_sync();
+            cnt -= nb;
         }
-        wave_sync();
-        bwd_drain<MODE, RAYS>(srec, grow, tth, tph, pd, prho, pacc, queue, cnt, gray, np_, r0, dr, nr, cdt, f0log2,
-                              rscale);
+        if (ccnt > 0) {
+            wave_sync();
+            bwd_chunks<MODE, RAYS>(chq, ccnt, pdat, grow, tth, tph, pacc, rows, gray, np_, nr, r0, dr, inv_dr, cdt,
+                                   f0log2, rscale);
+        }
         wave_sync();
         // per-pair chain for this wave's pair (Gaussian gi, wall point p)
         if (active) {

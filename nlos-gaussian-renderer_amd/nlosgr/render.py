@@ -25,6 +25,7 @@ class RenderConfig:
     c_deltaT: float = 1.0
     ray_scale: float = 1.0
     nsplit: int = 0
+    flags: int = 0               # ablation / diagnostics only (0 in production)
 
 
 def _as_f32(t):
@@ -50,7 +51,7 @@ def _structs(mu, scaling, rotation, opacity, features, geo, cfg):
                        _lib.ptr(geo.cos_theta), _lib.ptr(geo.sin_phi), _lib.ptr(geo.cos_phi),
                        _lib.ptr(geo.grid_lin), _lib.ptr(geo.hscale), _lib.ptr(geo.r), _lib.ptr(geo.att))
     o = _lib.Options(_lib.MODES[cfg.mode], float(cfg.cutoff), float(cfg.c_deltaT), float(cfg.ray_scale),
-                     int(cfg.nsplit), 0)
+                     int(cfg.nsplit), int(cfg.flags))
     return g, gs, o
 
 

@@ -1,0 +1,25 @@
+"""Ablation timing of the forward kernel phases (diagnostic; opt.flags bits)."""
+import sys, os, time, json
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, 'nlos-gaussian-renderer_amd')); sys.path.insert(0, ROOT)
+import torch, dataclasses
+from nlosgr import GaussianParams, features_flat
+from nlosgr.volume import Scene, make_config
+from nlosgr.render import render_forward
+cfgname = sys.argv[1] if len(sys.argv) > 1 else 'C3'
+sizes = {'C3': (100_000, 128, 1024), 'S1': (20_000, 32, 512)}
+ng, H, T = sizes[cfgname]
+dev = torch.device('cuda:0')
+scene = Scene(H=H, W=H, T=T, ns=32)
+m = GaussianParams.synthetic(ng, 3, preset="cuda", device=dev, seed=0)
+geo = scene.geometry(dev, "cuda")
+f = features_flat(m).detach()
+args = (m._mu.detach(), m._scaling.detach(), m._rotation.detach(), m._opacity.detach(), f, geo)
+base = make_config(m, scene, cutoff=3.0)
+res = {}
+for flags in (0, 1, 2, 3):
+    cfg = dataclasses.replace(base, flags=flags)
+    render_forward(*args, cfg); torch.cuda.synchronize()
+    t0 = time.perf_counter(); render_forward(*args, cfg); torch.cuda.synchronize()
+    res[flags] = (time.perf_counter() - t0) * 1000
+print(json.dumps({'config': cfgname, 'fwd_ms_by_flags': res}))
