@@ -32,6 +32,7 @@ CONFIGS = {
 }
 PEAK_HBM_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 PEAK_FP32_TFLOPS = 157.3       # FP32 vector peak (the path has no MFMA shape)
+FLOP_PER_EVAL = {"fwd": 36, "bwd": 100}   # SURVEY §8d convention (FMA = 2, exp = 1)
 
 
 def param_bytes(deg):
@@ -39,35 +40,54 @@ def param_bytes(deg):
 
 
 def cpu_baseline(cfg_name, seed=0):
-    """Time the CPU oracle (dense restatement of the reference, cuda preset) on a bounded sample of
-    the same workload: 1 wall point x G_SAMPLE of the Ng Gaussians x the full Ns^2 x T sample grid,
-    fwd+bwd; extrapolated linearly (cost is linear in Gaussians and in wall points)."""
+    """Time the CPU oracle (dense restatement of the reference's torch path, cuda preset) on a
+    bounded sample of the same workload: 1 wall point x G_SAMPLE of the Ng Gaussians x the full
+    Ns^2 x T sample grid, fwd+bwd, in chunks of 32 Gaussians (bounded memory); extrapolated
+    linearly (the dense cost is linear in Gaussians and in wall points)."""
+    from nlosgr.model import GaussianParams
     from nlosgr.volume import Scene
     from oracle import torch_ref as R
     ng, H, W, T, ns, _ = CONFIGS[cfg_name]
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
     torch.set_num_threads(threads)
     scene = Scene(H=H, W=W, T=T, ns=ns)
-    g_sample = max(1, min(ng, int(os.environ.get("NLOSGR_CPU_SAMPLE_G", "16"))))
-    from nlosgr.model import GaussianParams
+    g_sample = max(1, min(ng, int(os.environ.get("NLOSGR_CPU_SAMPLE_G", "160"))))
     m = GaussianParams.synthetic(ng, 3, preset="cuda", device="cpu", seed=seed)
-    sl = slice(0, g_sample)
-    P = R.Params(m._mu.detach()[sl], m._scaling.detach()[sl], m._rotation.detach()[sl], m._opacity.detach()[sl],
-                 m._features_dc.detach()[sl], m._features_rest.detach()[sl], 3)
     walls = scene.walls("cpu")
-    box = scene.box("cpu")
     p = walls[(H // 2) * W + W // 2]
-    tab = R.sample_tables(p, box, ns, scene.start, scene.end, scene.c, scene.deltaT)
-    # warm-up on a small radial slice, then the timed full sample
+    tab = R.sample_tables(p, scene.box("cpu"), ns, scene.start, scene.end, scene.c, scene.deltaT)
     t0 = time.perf_counter()
-    _, h = R.render_wallpoint(P, p, tab, 0.5, scene.c, scene.deltaT, preset="cuda", mode="noocl")
-    (h * h).sum().backward()
+    for g0 in range(0, g_sample, 32):
+        sl = slice(g0, min(g_sample, g0 + 32))
+        P = R.Params(*(t.detach()[sl].clone() for t in (m._mu, m._scaling, m._rotation, m._opacity,
+                                                        m._features_dc, m._features_rest)), 3)
+        _, h = R.render_wallpoint(P, p, tab, 0.5, scene.c, scene.deltaT, preset="cuda", mode="noocl")
+        (h * h).sum().backward()
     t = time.perf_counter() - t0
     per_volume = t * (ng / g_sample) * (H * W)
     return {"value": 1.0 / per_volume, "unit": "volumes/s", "cores": threads, "kind": "port",
             "sample": f"oracle/torch_ref dense (cuda preset) fwd+bwd of 1 wall point x {g_sample} of {ng} "
                       f"Gaussians x {ns}x{ns}x{T} samples = {t:.2f} s on {threads} threads; "
-                      f"extrapolated x{ng // g_sample} Gaussians x{H * W} wall points"}
+                      f"extrapolated x{ng / g_sample:g} Gaussians x{H * W} wall points"}
+
+
+def pmc_traffic(cfg_name, kernels):
+    """HBM bytes per launch of `kernels` (name substrings) from the newest committed
+    profiles/r*_<cfg>_traffic.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE passes of this bench,
+    scripts/prof_c3.sh + scripts/summarize_prof.py), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{cfg_name.lower()}_traffic.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        rec = json.load(f)["kernels"]
+    total = 0.0
+    for sub in kernels:
+        hits = [v["hbm_bytes_per_launch"] for k, v in rec.items() if sub in k]
+        if not hits:
+            return None, None
+        total += max(hits)
+    return total, os.path.relpath(files[-1], ROOT)
 
 
 def main():
@@ -153,16 +173,27 @@ def main():
     ms_per_step = elapsed * 1000.0 / a.steps
     volumes_per_s = world * a.steps / elapsed
 
-    # roofline of the dominant kernel (algorithmic HBM bytes / measured launch time)
+    # roofline of the dominant phase (algorithmic HBM bytes / measured launch time)
     pb = param_bytes(3)
     V = 4 * H * W * T
     fwd_avg = sum(fwd_ms) / len(fwd_ms)
     bwd_avg = sum(bwd_ms) / len(bwd_ms) if bwd_ms else 0.0
     if bwd_avg >= fwd_avg:
-        dom, dom_ms, dom_bytes = "nlosgr bwd (preprocess+bwd_kernel+finish)", bwd_avg, 2 * ng * pb + V
+        dom, dom_ms, dom_bytes = "bwd", bwd_avg, 2 * ng * pb + V
+        kern = ("preprocess_kernel", "bwd_kernel", "finish_kernel")
     else:
-        dom, dom_ms, dom_bytes = "nlosgr fwd (preprocess+fwd_kernel)", fwd_avg, ng * pb + V
+        dom, dom_ms, dom_bytes = "fwd", fwd_avg, ng * pb + V
+        kern = ("preprocess_kernel", "fwd_kernel")
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
+    traffic, traffic_src = pmc_traffic(a.config, kern)
+    # secondary roofline: in-support evaluations (counting pass, untimed) x SURVEY FLOP convention
+    from nlosgr.render import count_support
+    pairs, rays, evals = count_support(*params, geo, cfg)
+    flops = evals * FLOP_PER_EVAL[dom]
+    valu = {"bound": "valu", "evaluations": evals, "pairs": pairs, "rays": rays,
+            "flop_per_eval": FLOP_PER_EVAL[dom], "achieved": flops / (dom_ms * 1e-3) / 1e12,
+            "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s"}
+    valu["frac"] = valu["achieved"] / PEAK_FP32_TFLOPS
     out = {
         "metric": "transient volumes/sec (fwd+bwd), 100k Gaussians → 128×128×1024 ToF bins"
         if a.config == "C3" else f"transient volumes/sec ({'fwd' if fwd_only else 'fwd+bwd'}) {a.config}",
@@ -175,9 +206,11 @@ def main():
                    "gaussians": ng, "wall": [H, W], "bins": T, "angular": ns, "cutoff": a.cutoff,
                    "parallelism": f"wall-replica x{world}, grad all-reduce" if world > 1 else "single GPU"},
         "phase_ms": {"fwd": fwd_avg, "bwd": bwd_avg},
-        "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                     "frac": achieved / PEAK_HBM_GBS, "traffic": None,
+        "roofline": {"bound": "hbm", "kernel": f"nlosgr {dom} ({' + '.join(kern)})", "achieved": achieved,
+                     "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS,
+                     "traffic": traffic, "traffic_source": traffic_src,
                      "algorithmic_bytes_per_launch": dom_bytes, "avg_launch_ms": dom_ms},
+        "roofline_valu": valu,
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         try:

@@ -112,6 +112,13 @@ int nlosgr_render_bwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo,
                       const float* grad_ray, float* d_mu, float* d_scaling, float* d_rotation,
                       float* d_opacity, float* d_features, void* hip_stream);
 
+/* Work count of one forward at opt->cutoff (no outputs written): counts (DEVICE, [3] uint64,
+ * overwritten) = {in-support (wall point, Gaussian) pairs, in-support rays (pair, i, j),
+ * in-support evaluations (pair, i, j, k)} — the unit of the VALU roofline. */
+int nlosgr_count_support(const nlosgr_gaussians* g, const nlosgr_geometry* geo,
+                         const nlosgr_options* opt, void* workspace, unsigned long long* counts,
+                         void* hip_stream);
+
 /* 3-sigma (sigma_scale) axis-aligned boxes [ng,6] = (min xyz, max xyz) under the preset's scale
  * convention (bbox_compute.cuh:23-71 for "cuda"; gaussian_model.py:140-178 for "torch"). */
 int nlosgr_bboxes(const nlosgr_gaussians* g, float sigma_scale, float* bboxes_out, void* hip_stream);

@@ -82,6 +82,7 @@ struct KArgs {
     const float* grad_ray;
     float* partial;  // [nsplit][ng][32]
     int nsplit;
+    unsigned long long* counts;  // optional [3]: pairs, segments, samples (nlosgr_count_support)
 };
 
 // ------------------------------------------------------------------------------------------
@@ -364,7 +365,8 @@ __device__ __forceinline__ Seg readlane_seg(const Seg& s, int l) {
 template <int MODE, bool DENSE, bool RAYS>
 __device__ __forceinline__ void fwd_rays(const unsigned* rayq, int cnt, const float* pdat, const float2* tth,
                                          const float2* tph, float* acc0, float* acc1, float* rout, int np_, int nr,
-                                         float mc2, float r0, float dr, float inv_dr, float rscale, float f0log2) {
+                                         float mc2, float r0, float dr, float inv_dr, float rscale, float f0log2,
+                                         int flags, unsigned& nseg, unsigned& nsamp) {
     const int lane = lane_id();
     Seg sg;
     bool pass = false;
@@ -389,6 +391,10 @@ __device__ __forceinline__ void fwd_rays(const unsigned* rayq, int cnt, const fl
         }
     }
     unsigned long long mask = __builtin_amdgcn_ballot_w64(pass);
+    if (flags & 4) {                         // diagnostics: records only, no drain
+        if (mask == 0x123456789ull) acc0[lane] += sg.al + sg.ga + sg.ls;
+        return;
+    }
     if (MODE == NLOSGR_MODE_NOOCL) {
         while (mask) {
             const int l0 = __builtin_ctzll(mask);
@@ -400,20 +406,29 @@ __device__ __forceinline__ void fwd_rays(const unsigned* rayq, int cnt, const fl
             const Seg b = readlane_seg(sg, l1);
             const int lenb = two ? b.len : 0;
             const int lmax = max(a.len, lenb);
+            nseg += 1 + (int)two;
+            nsamp += a.len + lenb;
             float* pa = acc0 + a.kl;
             float* pb = acc1 + b.kl;
+            // branch-free: histograms are padded by 64 bins, so every lane read-add-writes and lanes
+            // past a segment's end add 0 (gamma < 0, so the exponent of those lanes stays finite).
+            // a's window never leaves [a.kl, nr + 64); b's idle lanes are redirected into the pad.
+            const float sta = a.st, stb = two ? b.st : 0.f;
             float ta = (float)lane - a.ls, tb = (float)lane - b.ls;
             for (int lam = lane, m0 = 0; m0 < lmax; m0 += 64, lam += 64, ta += 64.f, tb += 64.f) {
-                const bool ia = lam < a.len, ib = lam < lenb;
-                const float va = ia ? fast_exp2(fmaf(a.ga, ta * ta, a.al)) : 0.f;
-                const float vb = ib ? fast_exp2(fmaf(b.ga, tb * tb, b.al)) : 0.f;
-                const float xa = ia ? pa[lam] : 0.f;
-                const float xb = ib ? pb[lam] : 0.f;
-                if (ia) pa[lam] = fmaf(a.st, va, xa);
-                if (ib) pb[lam] = fmaf(b.st, vb, xb);
+                const float ea = fast_exp2(fmaf(a.ga, ta * ta, a.al));
+                const float eb = fast_exp2(fmaf(b.ga, tb * tb, b.al));
+                const float va = lam < a.len ? ea : 0.f;
+                const float vb = lam < lenb ? eb : 0.f;
+                // lanes past b's end go to distinct pad bins (a.len may exceed b.len)
+                float* qb = lam < lenb ? pb + lam : acc1 + nr + lane;
+                const float xa = pa[lam];
+                const float xb = *qb;
+                pa[lam] = fmaf(sta, va, xa);
+                *qb = fmaf(stb, vb, xb);
                 if (RAYS) {
-                    if (ia) atomicAdd(rout + (size_t)a.ray * nr + a.kl + lam, rscale * va);
-                    if (ib) atomicAdd(rout + (size_t)b.ray * nr + b.kl + lam, rscale * vb);
+                    if (lam < a.len) atomicAdd(rout + (size_t)a.ray * nr + a.kl + lam, rscale * va);
+                    if (lam < lenb) atomicAdd(rout + (size_t)b.ray * nr + b.kl + lam, rscale * vb);
                 }
             }
         }
@@ -426,6 +441,8 @@ __device__ __forceinline__ void fwd_rays(const unsigned* rayq, int cnt, const fl
             mask &= mask - 1;
             const Seg a = readlane_seg(sg, l0);
             float* pa = acc0 + a.kl;
+            nseg += 1;
+            nsamp += a.len;
             float logT = (float)a.kl * f0log2;
             float ta = (float)lane - a.ls;
             for (int lam = lane, m0 = 0; m0 < a.len; m0 += 64, lam += 64, ta += 64.f) {
@@ -484,6 +501,7 @@ __global__ __launch_bounds__(kBlock) void fwd_kernel(KArgs k) {
     const float f0log2 = log2f(1.0f + 1e-7f);
     float* rout = RAYS ? k.ray_out + (size_t)p * nt * np_ * nr : nullptr;
     const float rscale = k.opt.ray_scale;
+    unsigned npair = 0, nseg = 0, nsamp = 0;
 
     for (int base = wave * 64; base < k.g.ng; base += kBlock) {
         const int gi = base + lane;
@@ -502,19 +520,27 @@ __global__ __launch_bounds__(kBlock) void fwd_kernel(KArgs k) {
         }
         wave_sync();
         int ci = P.i0, cj = P.j0, cnt = 0;
+        if (k.opt.flags & 2) more = false;   // diagnostics: pair setup only
+        npair += __builtin_popcountll(__builtin_amdgcn_ballot_w64(more));
         while (true) {
             enumerate<DENSE>(P, more, ci, cj, tth, tph, rayq, cnt);
             if (cnt == 0) break;
             wave_sync();
             const int nb = min(cnt, 64);
-            fwd_rays<MODE, DENSE, RAYS>(rayq, nb, pdat, tth, tph, acc0, acc1, rout, np_, nr, mc2, r0, dr, inv_dr,
-                                        rscale, f0log2);
+            if (!(k.opt.flags & 1))          // diagnostics: skip segment records + drain
+                fwd_rays<MODE, DENSE, RAYS>(rayq, nb, pdat, tth, tph, acc0, acc1, rout, np_, nr, mc2, r0, dr, inv_dr,
+                                            rscale, f0log2, k.opt.flags, nseg, nsamp);
             wave_sync();
             if (lane < cnt - nb) rayq[lane] = rayq[nb + lane];
             wave_sync();
             cnt -= nb;
         }
         wave_sync();
+    }
+    if (k.counts && lane == 0) {
+        atomicAdd(k.counts, (unsigned long long)npair);
+        atomicAdd(k.counts + 1, (unsigned long long)nseg);
+        atomicAdd(k.counts + 2, (unsigned long long)nsamp);
     }
     __syncthreads();
     if (k.hist_out) {
@@ -1062,6 +1088,33 @@ void launch_preprocess(const nlosgr_gaussians* g, GaussRec* recs, hipStream_t s)
         hipLaunchKernelGGL(preprocess_kernel<NLOSGR_PRESET_CUDA>, dim3(nb), dim3(kBlock), 0, s, *g, recs);
 }
 
+int run_fwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_options* opt, void* workspace,
+            float* hist_out, float* ray_out, unsigned long long* counts, hipStream_t s) {
+    if (g->ng > 0 && !workspace) return set_err(NLOSGR_E_INVALID, "workspace is null");
+    KArgs ka;
+    memset(&ka, 0, sizeof(ka));
+    ka.g = *g; ka.geo = *geo; ka.opt = *opt;
+    ka.recs = (const GaussRec*)workspace;
+    ka.hist_out = hist_out; ka.ray_out = ray_out;
+    ka.counts = counts;
+    if (g->ng > 0) {
+        launch_preprocess(g, (GaussRec*)workspace, s);
+        HIPCHK(hipGetLastError());
+    }
+    const size_t shm = (size_t)FwdLayout(geo->nr, geo->nt, geo->np).total * sizeof(float);
+    const bool dense = !(opt->cutoff > 0.f);
+    const bool rays = ray_out != nullptr;
+    if (g->preset == NLOSGR_PRESET_TORCH) {
+        if (opt->mode == NLOSGR_MODE_NOOCL) dispatch_fwd<0, 0>(ka, dense, rays, shm, s);
+        else dispatch_fwd<0, 1>(ka, dense, rays, shm, s);
+    } else {
+        if (opt->mode == NLOSGR_MODE_NOOCL) dispatch_fwd<1, 0>(ka, dense, rays, shm, s);
+        else dispatch_fwd<1, 1>(ka, dense, rays, shm, s);
+    }
+    HIPCHK(hipGetLastError());
+    return NLOSGR_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1079,32 +1132,21 @@ size_t nlosgr_workspace_bytes(const nlosgr_gaussians* g, const nlosgr_geometry* 
 
 int nlosgr_render_fwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_options* opt,
                       void* workspace, float* hist_out, float* ray_out, void* hip_stream) {
-    int rc = validate(g, geo, opt);
+    const int rc = validate(g, geo, opt);
     if (rc) return rc;
     if (geo->nwall == 0 || (!hist_out && !ray_out)) return NLOSGR_OK;
-    if (g->ng > 0 && !workspace) return set_err(NLOSGR_E_INVALID, "workspace is null");
+    return run_fwd(g, geo, opt, workspace, hist_out, ray_out, nullptr, (hipStream_t)hip_stream);
+}
+
+int nlosgr_count_support(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_options* opt,
+                         void* workspace, unsigned long long* counts, void* hip_stream) {
+    const int rc = validate(g, geo, opt);
+    if (rc) return rc;
+    if (!counts) return set_err(NLOSGR_E_INVALID, "counts is null");
     hipStream_t s = (hipStream_t)hip_stream;
-    KArgs ka;
-    memset(&ka, 0, sizeof(ka));
-    ka.g = *g; ka.geo = *geo; ka.opt = *opt;
-    ka.recs = (const GaussRec*)workspace;
-    ka.hist_out = hist_out; ka.ray_out = ray_out;
-    if (g->ng > 0) {
-        launch_preprocess(g, (GaussRec*)workspace, s);
-        HIPCHK(hipGetLastError());
-    }
-    const size_t shm = (size_t)FwdLayout(geo->nr, geo->nt, geo->np).total * sizeof(float);
-    const bool dense = !(opt->cutoff > 0.f);
-    const bool rays = ray_out != nullptr;
-    if (g->preset == NLOSGR_PRESET_TORCH) {
-        if (opt->mode == NLOSGR_MODE_NOOCL) dispatch_fwd<0, 0>(ka, dense, rays, shm, s);
-        else dispatch_fwd<0, 1>(ka, dense, rays, shm, s);
-    } else {
-        if (opt->mode == NLOSGR_MODE_NOOCL) dispatch_fwd<1, 0>(ka, dense, rays, shm, s);
-        else dispatch_fwd<1, 1>(ka, dense, rays, shm, s);
-    }
-    HIPCHK(hipGetLastError());
-    return NLOSGR_OK;
+    HIPCHK(hipMemsetAsync(counts, 0, 3 * sizeof(unsigned long long), s));
+    if (geo->nwall == 0) return NLOSGR_OK;
+    return run_fwd(g, geo, opt, workspace, nullptr, nullptr, counts, s);
 }
 
 int nlosgr_render_bwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_options* opt,

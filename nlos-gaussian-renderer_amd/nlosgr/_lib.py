@@ -40,8 +40,8 @@ class Options(ctypes.Structure):
 
 
 # every symbol include/nlosgr.h declares (tests check the exports against this list)
-EXPORTS = ["nlosgr_workspace_bytes", "nlosgr_render_fwd", "nlosgr_render_bwd", "nlosgr_bboxes",
-           "nlosgr_last_error", "nlosgr_abi_version"]
+EXPORTS = ["nlosgr_workspace_bytes", "nlosgr_render_fwd", "nlosgr_render_bwd", "nlosgr_count_support",
+           "nlosgr_bboxes", "nlosgr_last_error", "nlosgr_abi_version"]
 
 _lib = None
 _load_error = None
@@ -63,6 +63,8 @@ def load():
     lib.nlosgr_render_fwd.restype = ctypes.c_int
     lib.nlosgr_render_bwd.argtypes = [PG, PGEO, POPT, _P, _P, _P, _P, _P, _P, _P, _P, _P]
     lib.nlosgr_render_bwd.restype = ctypes.c_int
+    lib.nlosgr_count_support.argtypes = [PG, PGEO, POPT, _P, _P, _P]
+    lib.nlosgr_count_support.restype = ctypes.c_int
     lib.nlosgr_bboxes.argtypes = [PG, ctypes.c_float, _P, _P]
     lib.nlosgr_bboxes.restype = ctypes.c_int
     lib.nlosgr_last_error.argtypes = []

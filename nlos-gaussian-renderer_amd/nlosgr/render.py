@@ -95,6 +95,19 @@ def render_backward(mu, scaling, rotation, opacity, features, geo, cfg, grad_his
     return d_mu, d_s, d_q, d_o, d_f
 
 
+def count_support(mu, scaling, rotation, opacity, features, geo, cfg):
+    """(pairs, rays, evaluations) in support at cfg.cutoff for one forward: the work unit of the
+    VALU roofline.  Dense (cutoff <= 0) counts every sample."""
+    lib = _lib.load()
+    dev = mu.device
+    mu, scaling, rotation, opacity, features = [_as_f32(t) for t in (mu, scaling, rotation, opacity, features)]
+    g, gs, o = _structs(mu, scaling, rotation, opacity, features, geo, cfg)
+    ws = _workspace(lib, g, gs, o, dev)
+    counts = torch.zeros(3, dtype=torch.int64, device=dev)
+    _lib.check(lib.nlosgr_count_support(g, gs, o, _lib.ptr(ws), _lib.ptr(counts), _lib.stream_handle(dev)))
+    return tuple(int(v) for v in counts.cpu())
+
+
 class RenderFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, mu, scaling, rotation, opacity, features, geo, cfg, want_hist, want_rays):

@@ -280,6 +280,19 @@ def render_volume(P, walls, box, Y, ns, start, end, c, deltaT, **kw):
     return torch.stack(hs)
 
 
+def count_support(P, walls, box, ns, start, end, c, deltaT, preset="cuda", mc=3.0, mod=1.0):
+    """Number of in-support evaluations (wall point, Gaussian, ray, bin) with Mahalanobis² ≤ mc²
+    and albedo > 0 — the work unit of SURVEY §8d (not a reference function; it counts the
+    nonzero terms of the gaussian_pdf × albedo product the reference sums)."""
+    n = 0
+    for w in range(walls.shape[0]):
+        tab = sample_tables(walls[w], box, ns, start, end, c, deltaT)
+        pdf = gaussian_pdf(tab["input_points"][:, 0:3], P, preset, mod, mc)
+        live = (albedo(P, walls[w], preset) > 0).float()
+        n += int(((pdf > 0).float() * live).sum())
+    return n
+
+
 def mse_loss(hist, target):
     """compute_loss: MSELoss(mean) vs target (already × gt_times), nlos_helpers.py:323-327."""
     loss = torch.mean((hist - target) ** 2)

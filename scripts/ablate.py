@@ -17,7 +17,7 @@ f = features_flat(m).detach()
 args = (m._mu.detach(), m._scaling.detach(), m._rotation.detach(), m._opacity.detach(), f, geo)
 base = make_config(m, scene, cutoff=3.0)
 res = {}
-for flags in (0, 1, 2, 3):
+for flags in (0, 4, 1, 2):
     cfg = dataclasses.replace(base, flags=flags)
     render_forward(*args, cfg); torch.cuda.synchronize()
     t0 = time.perf_counter(); render_forward(*args, cfg); torch.cuda.synchronize()

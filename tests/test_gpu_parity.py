@@ -134,3 +134,38 @@ def test_cutoff_converges_to_dense():
             errs.append(((h - dense).norm() / dense.norm()).item())
     assert errs[0] < 5e-2 and errs[1] < 3e-3 and errs[2] < 1e-4 and errs[3] < 2e-6, errs
     assert all(errs[i + 1] <= errs[i] for i in range(3)), errs
+
+
+@pytest.mark.parametrize("preset", ["torch", "cuda"])
+def test_count_support_vs_oracle(preset):
+    """The kernel's work count (pairs/rays/evaluations in support) vs the oracle's count of nonzero
+    masked-pdf terms; dense mode counts every sample of every live pair exactly."""
+    from nlosgr import GaussianParams, features_flat
+    from nlosgr.geometry import build_geometry, relay_wall_grid, volume_box_point
+    from nlosgr.render import RenderConfig, count_support
+    from oracle import torch_ref as R
+    dev = torch.device("cuda:0")
+    ng, deg, ns, T = 40, 3, 8, 48
+    c, deltaT = 1.0, 1.28 / T
+    start, end = T // 8, T // 8 + T
+    model = GaussianParams.synthetic(ng, deg, preset=preset, device=dev, seed=7)
+    if preset == "cuda":
+        with torch.no_grad():
+            model._scaling.add_(1.2)
+    walls = relay_wall_grid(2, 2, device=dev)
+    box = volume_box_point((0.0, 0.5, 0.0), 0.5, dev)
+    geo = build_geometry(walls, box, ns, start, end, c, deltaT, 0.5, preset, "noocl")
+    args = (model._mu, model._scaling, model._rotation, model._opacity, features_flat(model), geo)
+    cpu = lambda t: t.detach().cpu()
+    P = R.Params(cpu(model._mu), cpu(model._scaling), cpu(model._rotation), cpu(model._opacity),
+                 cpu(model._features_dc), cpu(model._features_rest), deg)
+    live = sum(int((R.albedo(P, w, preset) > 0).sum()) for w in cpu(walls))
+    cfg = RenderConfig(preset=preset, mode="noocl", sh_degree=deg, cutoff=0.0, c_deltaT=c * deltaT)
+    pairs, rays, evals = count_support(*args, cfg)
+    assert pairs == live and rays == live * ns * ns and evals == live * ns * ns * T
+    mc = 3.0
+    cfg = RenderConfig(preset=preset, mode="noocl", sh_degree=deg, cutoff=mc, c_deltaT=c * deltaT)
+    _, _, evals = count_support(*args, cfg)
+    ref = R.count_support(P, cpu(walls), cpu(box), ns, start, end, c, deltaT, preset, mc)
+    # boundary samples (m2 within fp32 rounding of mc^2) may flip
+    assert abs(evals - ref) <= max(2, 1e-3 * ref), (evals, ref)
