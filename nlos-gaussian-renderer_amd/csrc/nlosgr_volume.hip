@@ -320,151 +320,92 @@ __device__ __forceinline__ void enumerate(const Pair& P, bool& more, int& ci, in
     }
 }
 
+// ------------------------------------------------------------------------------------------
+// forward
+// ------------------------------------------------------------------------------------------
+// Lane-serial drain: lane = one ray segment, walking its bins kSteps at a time and adding each
+// value into the wave-private LDS histogram with a plain read-add-write.  At step m every lane
+// touches bin pos + m, so the adds of one instruction hit distinct addresses whenever the lanes'
+// start bins differ — guaranteed per round by a claim table (owner[pos] = lane; losers retry
+// next round).  Lanes that did not win, or ran past their segment, point at private pad bins
+// and add 0, so the step body is branch-free.  Idle lanes are refilled from the ray queue.
+constexpr int kSteps = 8;      // bins per lane per drain round
+constexpr int kRefill = 24;    // refill once this many lanes are idle (or the queue is final)
+
 struct FwdLayout {
-    int acc0, acc1, pdat, rayq, wave_stride, total;
+    int hist, owner, rayq, wave_stride, total;  // offsets in floats
     __host__ __device__ FwdLayout(int nr, int nt, int np_) {
         const int off = al4(2 * (nt + np_));  // float2 theta table [nt], float2 phi table [np]
-        acc0 = 0;                             // two wave-private histograms (alternating segments)
-        acc1 = al4(nr + 64);
-        pdat = acc1 + al4(nr + 64);           // [64][kPD]
-        rayq = pdat + 64 * kPD;               // uint [kRQ]
+        hist = 0;                             // [nr + kSteps] bins + [kSteps + 64] pad bins
+        owner = al4(nr + 2 * kSteps + 64);    // u8 [nr] claim table
+        rayq = owner + al4((nr + 3) / 4);     // uint [kRQ] ring
         wave_stride = al4(rayq + kRQ);
-        acc0 += off; acc1 += off; pdat += off; rayq += off;
+        hist += off; owner += off; rayq += off;
         total = off + kWaves * wave_stride;
     }
 };
 
-// ------------------------------------------------------------------------------------------
-// forward
-// ------------------------------------------------------------------------------------------
-// Segment record of one (pair, ray): value(lam) = exp2(al + ga (lam - ls)^2) at bin kl + lam,
-// lam in [0, len); histogram weight st = sin(theta_i).
-struct Seg {
-    float al, ga, ls, st, sc, wc;  // sc = sigma c dT, wc = w c dT (netf)
-    int kl, len, ray;
+// per-lane drain state (one segment)
+struct Drain {
+    int pos, rem;     // next bin, bins left
+    float t;          // pos - ks (bin offset from the closest approach)
+    float ga, al;     // log2 value(t) = ga t^2 + al   (noocl: al includes log2 w [+ log2 sin theta])
+    float st;         // sin(theta_i) (kept separate only when per-ray outputs are written)
+    float sc, lwc, logT;  // netf: sigma c dT, log2(w c dT), log2 T at pos
+    int rbase;        // RAYS: ray * nr
 };
 
-__device__ __forceinline__ Seg readlane_seg(const Seg& s, int l) {
-    Seg r;
-    r.al = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(s.al), l));
-    r.ga = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(s.ga), l));
-    r.ls = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(s.ls), l));
-    r.st = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(s.st), l));
-    r.sc = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(s.sc), l));
-    r.wc = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(s.wc), l));
-    r.kl = __builtin_amdgcn_readlane(s.kl, l);
-    r.len = __builtin_amdgcn_readlane(s.len, l);
-    r.ray = __builtin_amdgcn_readlane(s.ray, l);
-    return r;
+template <int MODE, bool DENSE, bool RAYS>
+__device__ __forceinline__ bool drain_setup(const float* A, const float* u0, float lw, float sc, float lwc,
+                                            float2 th, float2 ph, int i, int j, int np_, int nr, float mc2,
+                                            float r0, float dr, float inv_dr, float f0log2, Drain& d) {
+    Ray R;
+    if (!ray_setup<DENSE>(A, u0, th.x * ph.x, th.x * ph.y, th.y, mc2, r0, inv_dr, nr, R)) return false;
+    d.pos = R.kl;
+    d.rem = R.kh - R.kl + 1;
+    d.t = (float)R.kl - R.ks;
+    d.ga = -kHalfLog2e * R.a * dr * dr;
+    if (MODE == NLOSGR_MODE_NOOCL) {
+        d.al = fmaf(-kHalfLog2e, R.m2min, lw);
+        if (!RAYS) d.al += flog2(th.x);
+        d.st = th.x;
+    } else {
+        d.al = -kHalfLog2e * R.m2min;
+        d.sc = sc;
+        d.lwc = lwc;
+        d.logT = (float)R.kl * f0log2;
+        d.st = th.x;
+    }
+    d.rbase = (i * np_ + j) * nr;
+    return true;
 }
 
-// lane = ray-queue entry: exact support test + segment record; then the wave walks the passing
-// segments (2 at a time, alternating histogram copies so two read-add-writes are in flight) with
-// lane = bin.  Plain LDS read/add/write: each instruction touches 64 distinct addresses of a
-// wave-private histogram, so it is race-free and rounds to nearest.
-template <int MODE, bool DENSE, bool RAYS>
-__device__ __forceinline__ void fwd_rays(const unsigned* rayq, int cnt, const float* pdat, const float2* tth,
-                                         const float2* tph, float* acc0, float* acc1, float* rout, int np_, int nr,
-                                         float mc2, float r0, float dr, float inv_dr, float rscale, float f0log2,
-                                         int flags, unsigned& nseg, unsigned& nsamp) {
+// Candidate enumeration (lane = pair): quadric test only; passing (pair, ray) entries are appended
+// to the ray queue ring at qbase + cnt.  Returns when cnt >= 64 or every lane exhausted its box.
+template <bool DENSE>
+__device__ __forceinline__ void enumerate_ring(const Pair& P, bool& more, int& ci, int& cj, const float2* tth,
+                                               const float2* tph, unsigned* rayq, int qbase, int& cnt) {
     const int lane = lane_id();
-    Seg sg;
-    bool pass = false;
-    if (lane < cnt) {
-        const unsigned e = rayq[lane];
-        const int slot = e & 0xFF, i = (e >> 8) & 0xFFF, j = e >> 20;
-        PairLite q;
-        load_pair(pdat, slot, q);
-        const float2 th = tth[i], ph = tph[j];
-        Ray R;
-        if (ray_setup<DENSE>(q.A, q.u0, th.x * ph.x, th.x * ph.y, th.y, mc2, r0, inv_dr, nr, R)) {
-            pass = true;
-            sg.al = fmaf(-kHalfLog2e, R.m2min, MODE == NLOSGR_MODE_NOOCL ? q.lw : 0.f);
-            sg.ga = -kHalfLog2e * R.a * dr * dr;
-            sg.ls = R.ks - (float)R.kl;
-            sg.st = th.x;
-            sg.sc = q.sigma;
-            sg.wc = q.w;
-            sg.kl = R.kl;
-            sg.len = R.kh - R.kl + 1;
-            sg.ray = i * np_ + j;
-        }
-    }
-    unsigned long long mask = __builtin_amdgcn_ballot_w64(pass);
-    if (flags & 4) {                         // diagnostics: records only, no drain
-        if (mask == 0x123456789ull) acc0[lane] += sg.al + sg.ga + sg.ls;
-        return;
-    }
-    if (MODE == NLOSGR_MODE_NOOCL) {
-        while (mask) {
-            const int l0 = __builtin_ctzll(mask);
-            mask &= mask - 1;
-            const bool two = mask != 0;
-            const int l1 = two ? __builtin_ctzll(mask) : l0;
-            if (two) mask &= mask - 1;
-            const Seg a = readlane_seg(sg, l0);
-            const Seg b = readlane_seg(sg, l1);
-            const int lenb = two ? b.len : 0;
-            const int lmax = max(a.len, lenb);
-            nseg += 1 + (int)two;
-            nsamp += a.len + lenb;
-            float* pa = acc0 + a.kl;
-            float* pb = acc1 + b.kl;
-            // branch-free: histograms are padded by 64 bins, so every lane read-add-writes and lanes
-            // past a segment's end add 0 (gamma < 0, so the exponent of those lanes stays finite).
-            // a's window never leaves [a.kl, nr + 64); b's idle lanes are redirected into the pad.
-            const float sta = a.st, stb = two ? b.st : 0.f;
-            float ta = (float)lane - a.ls, tb = (float)lane - b.ls;
-            for (int lam = lane, m0 = 0; m0 < lmax; m0 += 64, lam += 64, ta += 64.f, tb += 64.f) {
-                const float ea = fast_exp2(fmaf(a.ga, ta * ta, a.al));
-                const float eb = fast_exp2(fmaf(b.ga, tb * tb, b.al));
-                const float va = lam < a.len ? ea : 0.f;
-                const float vb = lam < lenb ? eb : 0.f;
-                // lanes past b's end go to distinct pad bins (a.len may exceed b.len)
-                float* qb = lam < lenb ? pb + lam : acc1 + nr + lane;
-                const float xa = pa[lam];
-                const float xb = *qb;
-                pa[lam] = fmaf(sta, va, xa);
-                *qb = fmaf(stb, vb, xb);
-                if (RAYS) {
-                    if (lam < a.len) atomicAdd(rout + (size_t)a.ray * nr + a.kl + lam, rscale * va);
-                    if (lam < lenb) atomicAdd(rout + (size_t)b.ray * nr + b.kl + lam, rscale * vb);
-                }
+    while (__builtin_amdgcn_ballot_w64(more)) {
+        bool pass = false;
+        unsigned e = 0;
+        if (more) {
+            const float2 th = tth[ci], ph = tph[cj];
+            if (DENSE || quadric(P.M, th.x * ph.x, th.x * ph.y, th.y) >= 0.f) {
+                pass = true;
+                e = pack_ray(lane, ci, cj);
             }
+            if (++cj > P.j1) { cj = P.j0; ++ci; }
+            more = ci <= P.i1;
         }
-    } else {
-        // netf: T_k = prod_{k'<k} (exp(-sigma pdf c dT) + 1e-7) front-to-back along the ray
-        // (gaussian_model.py:317-321) as an exclusive log-domain prefix scan across the 64 lanes of
-        // each window, carried between windows; value = w c dT pdf T.
-        while (mask) {
-            const int l0 = __builtin_ctzll(mask);
-            mask &= mask - 1;
-            const Seg a = readlane_seg(sg, l0);
-            float* pa = acc0 + a.kl;
-            nseg += 1;
-            nsamp += a.len;
-            float logT = (float)a.kl * f0log2;
-            float ta = (float)lane - a.ls;
-            for (int lam = lane, m0 = 0; m0 < a.len; m0 += 64, lam += 64, ta += 64.f) {
-                const bool in = lam < a.len;
-                const float pdf = in ? fast_exp2(fmaf(a.ga, ta * ta, a.al)) : 0.f;
-                const float lf = in ? flog2(__expf(-a.sc * pdf) + 1e-7f) : 0.f;
-                float incl = lf;
-#pragma unroll
-                for (int o = 1; o < 64; o <<= 1) {
-                    const float u = __shfl_up(incl, o);
-                    if (lane >= o) incl += u;
-                }
-                if (in) {
-                    const float val = a.wc * pdf * fast_exp2(logT + (incl - lf));
-                    pa[lam] += a.st * val;
-                    if (RAYS) atomicAdd(rout + (size_t)a.ray * nr + a.kl + lam, rscale * val);
-                }
-                logT += __shfl(incl, 63);
-            }
-        }
+        const unsigned long long m = __builtin_amdgcn_ballot_w64(pass);
+        if (pass) rayq[(qbase + cnt + lanes_below(m)) & (kRQ - 1)] = e;
+        cnt += __popcll(m);
+        if (cnt >= 64) return;
     }
 }
+
+__device__ __forceinline__ void compiler_fence() { __asm__ __volatile__("" ::: "memory"); }
 
 template <int PRESET, int MODE, bool DENSE, bool RAYS>
 __global__ __launch_bounds__(kBlock) void fwd_kernel(KArgs k) {
@@ -475,9 +416,8 @@ __global__ __launch_bounds__(kBlock) void fwd_kernel(KArgs k) {
     float2* tph = tth + nt;
     const int wave = threadIdx.x >> 6, lane = lane_id();
     float* wb = smem + wave * L.wave_stride;
-    float* acc0 = wb + L.acc0;
-    float* acc1 = wb + L.acc1;
-    float* pdat = wb + L.pdat;
+    float* hist = wb + L.hist;
+    unsigned char* owner = reinterpret_cast<unsigned char*>(wb + L.owner);
     unsigned* rayq = reinterpret_cast<unsigned*>(wb + L.rayq);
     const int p = blockIdx.x;
 
@@ -485,10 +425,7 @@ __global__ __launch_bounds__(kBlock) void fwd_kernel(KArgs k) {
         tth[t] = make_float2(k.geo.sin_theta[(size_t)p * nt + t], k.geo.cos_theta[(size_t)p * nt + t]);
     for (int t = threadIdx.x; t < np_; t += blockDim.x)
         tph[t] = make_float2(k.geo.cos_phi[(size_t)p * np_ + t], k.geo.sin_phi[(size_t)p * np_ + t]);
-    for (int t = lane; t < nr + 64; t += 64) {
-        acc0[t] = 0.f;
-        acc1[t] = 0.f;
-    }
+    for (int t = lane; t < nr + 2 * kSteps + 64; t += 64) hist[t] = 0.f;
     __syncthreads();
 
     const float px = k.geo.wall[3 * p], py = k.geo.wall[3 * p + 1], pz = k.geo.wall[3 * p + 2];
@@ -501,56 +438,139 @@ __global__ __launch_bounds__(kBlock) void fwd_kernel(KArgs k) {
     const float f0log2 = log2f(1.0f + 1e-7f);
     float* rout = RAYS ? k.ray_out + (size_t)p * nt * np_ * nr : nullptr;
     const float rscale = k.opt.ray_scale;
-    unsigned npair = 0, nseg = 0, nsamp = 0;
+    const int flags = k.opt.flags;
+    const int pad = nr + kSteps + lane;       // this lane's private pad bins (non-winners)
+    unsigned npair = 0, nseg = 0;
+    unsigned long long nsamp = 0;
 
-    for (int base = wave * 64; base < k.g.ng; base += kBlock) {
-        const int gi = base + lane;
+    Drain d;
+    d.pos = 0; d.rem = 0; d.t = 0.f; d.ga = 0.f; d.al = 0.f; d.st = 0.f;
+    d.sc = 0.f; d.lwc = 0.f; d.logT = 0.f; d.rbase = 0;
+    bool act = false;
+    int qhead = 0, qcount = 0;
+
+    for (int base = wave * 64;; base += kBlock) {
+        const bool have = base < k.g.ng;      // wave-uniform
         Pair P;
-        float mu[3];
+        float lw = 0.f, sc = 0.f, lwc = 0.f;
         bool more = false;
+        int ci = 0, cj = 0;
         P.i0 = P.i1 = P.j0 = P.j1 = 0;
-        if (gi < k.g.ng) {
-            load_rec(k.recs[gi], P, mu);
-            pair_setup<PRESET, DENSE>(k, gi, mu, px, py, pz, lin, mc2, P);
-            more = (P.w > 0.f) && P.i0 <= P.i1 && P.j0 <= P.j1;
-            // netf keeps w, sigma scaled by c dT in the pair table
-            if (MODE == NLOSGR_MODE_NETF) { P.w *= cdt; P.sigma *= cdt; }
-            store_pair(pdat, lane, P, more ? flog2(P.w) : 0.f);
-            if (MODE == NLOSGR_MODE_NETF) { P.w /= cdt; P.sigma /= cdt; }
+        if (have) {
+            const int gi = base + lane;
+            if (gi < k.g.ng) {
+                float mu[3];
+                load_rec(k.recs[gi], P, mu);
+                pair_setup<PRESET, DENSE>(k, gi, mu, px, py, pz, lin, mc2, P);
+                more = (P.w > 0.f) && P.i0 <= P.i1 && P.j0 <= P.j1;
+                lw = more ? flog2(P.w) : 0.f;
+                sc = P.sigma * cdt;
+                lwc = more ? flog2(P.w * cdt) : 0.f;
+            }
+            if (flags & 2) more = false;      // diagnostics: pair setup only
+            npair += __builtin_popcountll(__builtin_amdgcn_ballot_w64(more));
+            ci = P.i0; cj = P.j0;
         }
-        wave_sync();
-        int ci = P.i0, cj = P.j0, cnt = 0;
-        if (k.opt.flags & 2) more = false;   // diagnostics: pair setup only
-        npair += __builtin_popcountll(__builtin_amdgcn_ballot_w64(more));
         while (true) {
-            enumerate<DENSE>(P, more, ci, cj, tth, tph, rayq, cnt);
-            if (cnt == 0) break;
+            if (qcount < 64 && __builtin_amdgcn_ballot_w64(more)) {
+                wave_sync();
+                enumerate_ring<DENSE>(P, more, ci, cj, tth, tph, rayq, qhead, qcount);
+                wave_sync();
+            }
+            const bool anymore = __builtin_amdgcn_ballot_w64(more) != 0;
+            const unsigned long long idle = __builtin_amdgcn_ballot_w64(!act);
+            const int nidle = __popcll(idle);
+            if (qcount > 0 && (nidle >= kRefill || !anymore)) {
+                // idle lane of rank r takes queue entry qhead + r; pair data come from lane `slot`
+                const int r = lanes_below(idle);
+                const bool take = !act && r < qcount;
+                const unsigned e = take ? rayq[(qhead + r) & (kRQ - 1)] : 0u;
+                const int slot = e & 0xFF, i = (e >> 8) & 0xFFF, j = e >> 20;
+                float A[9], u0[3];
+#pragma unroll
+                for (int c = 0; c < 9; ++c) A[c] = __shfl(P.A[c], slot);
+#pragma unroll
+                for (int c = 0; c < 3; ++c) u0[c] = __shfl(P.u0[c], slot);
+                const float lws = __shfl(lw, slot);
+                const float scs = MODE == NLOSGR_MODE_NETF ? __shfl(sc, slot) : 0.f;
+                const float lwcs = MODE == NLOSGR_MODE_NETF ? __shfl(lwc, slot) : 0.f;
+                bool got = false;
+                if (take && !(flags & 1)) {
+                    got = drain_setup<MODE, DENSE, RAYS>(A, u0, lws, scs, lwcs, tth[i], tph[j], i, j, np_, nr, mc2,
+                                                         r0, dr, inv_dr, f0log2, d);
+                    if (got) nsamp += (unsigned)d.rem;
+                    act = got && !(flags & 4);    // diagnostics: segment records only
+                }
+                nseg += __popcll(__builtin_amdgcn_ballot_w64(got));
+                const int ntake = min(nidle, qcount);
+                qhead = (qhead + ntake) & (kRQ - 1);
+                qcount -= ntake;
+            }
+            const bool anyact = __builtin_amdgcn_ballot_w64(act) != 0;
+            if (!anyact) {
+                if (!anymore && qcount == 0) break;
+                continue;
+            }
+            if (!anymore && qcount == 0 && have) break;   // next Gaussians; segments carry over
+            // claim distinct start bins
+            if (act) owner[d.pos] = (unsigned char)lane;
             wave_sync();
-            const int nb = min(cnt, 64);
-            if (!(k.opt.flags & 1))          // diagnostics: skip segment records + drain
-                fwd_rays<MODE, DENSE, RAYS>(rayq, nb, pdat, tth, tph, acc0, acc1, rout, np_, nr, mc2, r0, dr, inv_dr,
-                                            rscale, f0log2, k.opt.flags, nseg, nsamp);
+            const bool win = act && owner[d.pos] == (unsigned char)lane;
             wave_sync();
-            if (lane < cnt - nb) rayq[lane] = rayq[nb + lane];
-            wave_sync();
-            cnt -= nb;
+            const int remw = win ? d.rem : 0;
+            float* hb = hist + (win ? d.pos : pad);
+            float t = d.t;
+            float logT = d.logT;
+#pragma unroll
+            for (int m = 0; m < kSteps; ++m) {
+                const bool in = m < remw;
+                const float e2 = fmaf(d.ga, t * t, d.al);
+                float v;
+                if (MODE == NLOSGR_MODE_NOOCL) {
+                    const float pv = fast_exp2(e2);
+                    v = in ? pv : 0.f;
+                    if (RAYS) {
+                        if (in) atomicAdd(rout + d.rbase + d.pos + m, rscale * pv);
+                        v *= d.st;
+                    }
+                } else {
+                    const float pdf = fast_exp2(e2);
+                    const float lf = flog2(__expf(-d.sc * pdf) + 1e-7f);
+                    const float val = fast_exp2(d.lwc + logT) * pdf;
+                    if (RAYS && in) atomicAdd(rout + d.rbase + d.pos + m, rscale * val);
+                    logT += in ? lf : 0.f;
+                    v = in ? val * d.st : 0.f;
+                }
+                t += 1.f;
+                const float x = hb[m];
+                hb[m] = x + v;
+                compiler_fence();
+            }
+            if (win) {
+                d.t = t;
+                d.logT = logT;
+                d.pos += kSteps;
+                d.rem -= kSteps;
+                act = d.rem > 0;
+            }
         }
-        wave_sync();
+        if (!have) break;
     }
-    if (k.counts && lane == 0) {
-        atomicAdd(k.counts, (unsigned long long)npair);
-        atomicAdd(k.counts + 1, (unsigned long long)nseg);
-        atomicAdd(k.counts + 2, (unsigned long long)nsamp);
+    if (k.counts) {
+        unsigned long long ns = nsamp;
+        for (int o = 32; o > 0; o >>= 1) ns += __shfl_xor(ns, o);
+        if (lane == 0) {
+            atomicAdd(k.counts, (unsigned long long)npair);
+            atomicAdd(k.counts + 1, (unsigned long long)nseg);
+            atomicAdd(k.counts + 2, ns);
+        }
     }
     __syncthreads();
     if (k.hist_out) {
         const float hs = k.geo.hscale[p];
         for (int t = threadIdx.x; t < nr; t += blockDim.x) {
             float s = 0.f;
-            for (int w = 0; w < kWaves; ++w) {
-                const float* b = smem + w * L.wave_stride;
-                s += b[L.acc0 + t] + b[L.acc1 + t];
-            }
+            for (int w = 0; w < kWaves; ++w) s += smem[w * L.wave_stride + L.hist + t];
             k.hist_out[(size_t)p * nr + t] = s * k.geo.att[t] * hs;
         }
     }
