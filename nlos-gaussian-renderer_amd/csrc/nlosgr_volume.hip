@@ -267,57 +267,8 @@ __device__ __forceinline__ bool ray_setup(const float* A, const float* u0, float
 __host__ __device__ __forceinline__ int al4(int n) { return (n + 3) & ~3; }
 
 constexpr int kRQ = 128;      // ray queue capacity per wave (processed in batches of 64)
-constexpr int kPD = 16;       // floats of per-pair data in LDS: A[9], u0[3], w, sigma, log2 w, rho
-
-// per-wave pair table: written by lane = pair, read by lane = ray entry
-__device__ __forceinline__ void store_pair(float* pdat, int slot, const Pair& P, float lw) {
-    float4* d = reinterpret_cast<float4*>(pdat + slot * kPD);
-    d[0] = make_float4(P.A[0], P.A[1], P.A[2], P.A[3]);
-    d[1] = make_float4(P.A[4], P.A[5], P.A[6], P.A[7]);
-    d[2] = make_float4(P.A[8], P.u0[0], P.u0[1], P.u0[2]);
-    d[3] = make_float4(P.w, P.sigma, lw, P.rho);
-}
-
-struct PairLite {
-    float A[9], u0[3], w, sigma, lw, rho;
-};
-
-__device__ __forceinline__ void load_pair(const float* pdat, int slot, PairLite& q) {
-    const float4* s = reinterpret_cast<const float4*>(pdat + slot * kPD);
-    const float4 a = s[0], b = s[1], c = s[2], d = s[3];
-    q.A[0] = a.x; q.A[1] = a.y; q.A[2] = a.z; q.A[3] = a.w;
-    q.A[4] = b.x; q.A[5] = b.y; q.A[6] = b.z; q.A[7] = b.w;
-    q.A[8] = c.x; q.u0[0] = c.y; q.u0[1] = c.z; q.u0[2] = c.w;
-    q.w = d.x; q.sigma = d.y; q.lw = d.z; q.rho = d.w;
-}
-
 __device__ __forceinline__ unsigned pack_ray(int slot, int i, int j) {
     return (unsigned)slot | ((unsigned)i << 8) | ((unsigned)j << 20);
-}
-
-// Candidate enumeration (lane = pair): quadric test only; passing (pair, ray) go to the ray queue.
-// Returns when the queue holds >= 64 entries or every lane has exhausted its box.
-template <bool DENSE>
-__device__ __forceinline__ void enumerate(const Pair& P, bool& more, int& ci, int& cj, const float2* tth,
-                                          const float2* tph, unsigned* rayq, int& cnt) {
-    const int lane = lane_id();
-    while (__builtin_amdgcn_ballot_w64(more)) {
-        bool pass = false;
-        unsigned e = 0;
-        if (more) {
-            const float2 th = tth[ci], ph = tph[cj];
-            if (DENSE || quadric(P.M, th.x * ph.x, th.x * ph.y, th.y) >= 0.f) {
-                pass = true;
-                e = pack_ray(lane, ci, cj);
-            }
-            if (++cj > P.j1) { cj = P.j0; ++ci; }
-            more = ci <= P.i1;
-        }
-        const unsigned long long m = __builtin_amdgcn_ballot_w64(pass);
-        if (pass) rayq[cnt + lanes_below(m)] = e;
-        cnt += __popcll(m);
-        if (cnt >= 64) return;
-    }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -397,6 +348,31 @@ __device__ __forceinline__ void enumerate_ring(const Pair& P, bool& more, int& c
             }
             if (++cj > P.j1) { cj = P.j0; ++ci; }
             more = ci <= P.i1;
+        }
+        const unsigned long long m = __builtin_amdgcn_ballot_w64(pass);
+        if (pass) rayq[(qbase + cnt + lanes_below(m)) & (kRQ - 1)] = e;
+        cnt += __popcll(m);
+        if (cnt >= 64) return;
+    }
+}
+
+// enumerate_ring over explicit quadric/box registers (backward: the pair state is not kept)
+template <bool DENSE>
+__device__ __forceinline__ void enumerate_box(const float* M, int i1, int j0, int j1, bool& more, int& ci, int& cj,
+                                              const float2* tth, const float2* tph, unsigned* rayq, int qbase,
+                                              int& cnt) {
+    const int lane = lane_id();
+    while (__builtin_amdgcn_ballot_w64(more)) {
+        bool pass = false;
+        unsigned e = 0;
+        if (more) {
+            const float2 th = tth[ci], ph = tph[cj];
+            if (DENSE || quadric(M, th.x * ph.x, th.x * ph.y, th.y) >= 0.f) {
+                pass = true;
+                e = pack_ray(lane, ci, cj);
+            }
+            if (++cj > j1) { cj = j0; ++ci; }
+            more = ci <= i1;
         }
         const unsigned long long m = __builtin_amdgcn_ballot_w64(pass);
         if (pass) rayq[(qbase + cnt + lanes_below(m)) & (kRQ - 1)] = e;
@@ -579,22 +555,25 @@ __global__ __launch_bounds__(kBlock) void fwd_kernel(KArgs k) {
 // ------------------------------------------------------------------------------------------
 // backward
 // ------------------------------------------------------------------------------------------
-constexpr int kChunk = 32;   // segments are split into chunks of <= kChunk bins (lane-serial work)
+// Lane-serial backward drain: lane = one ray segment, kBSteps bins per round (the upstream
+// gradient reads of a round are issued together), sums S_n = sum H pdf kap^n in registers.  A
+// finished ray's closed-form result (dL/du0, dL/dv, dsigma, drho) is handed to the lane that owns
+// its pair: finished lanes claim owner[slot] with a round stamp, each pair lane gathers its
+// claimant's result with ds_bpermute and folds it into the Gaussian's register accumulators.
+// Losers keep their result and retry next round.  No LDS float atomics, no pair/row tables.
+constexpr int kBSteps = 8;
 
 struct BwdLayout {
-    int recs, wave_base, wave_stride, grow, tth, tph, pdat, pacc, rows, rayq, chq, red, total;
+    int wave_base, wave_stride, grow, tth, tph, rayq, owner, pdat, red, total;
     __host__ __device__ BwdLayout(int nr, int nt, int np_) {
-        recs = 0;                            // GaussRec [kNB] (20 floats each)
-        wave_base = al4(kNB * 20);
-        grow = 0;                            // [nr] upstream gradient row x att x hscale
-        tth = al4(nr);                       // float2 [nt]
+        wave_base = 0;
+        grow = 0;                            // [nr + kBSteps] upstream gradient x att x hscale, zero pad
+        tth = al4(nr + kBSteps);             // float2 [nt]
         tph = tth + al4(2 * nt);             // float2 [np]
-        pdat = tph + al4(2 * np_);           // [64][kPD] pair table
-        pacc = pdat + 64 * kPD;              // [64][16] per-pair accumulators
-        rows = pacc + 64 * 16;               // [64][16] per-chunk results (reduction staging)
-        rayq = rows + 64 * 16;               // uint [kRQ]
-        chq = rayq + kRQ;                    // uint2 [kRQ] chunk queue
-        wave_stride = al4(chq + 2 * kRQ);
+        rayq = tph + al4(2 * np_);           // uint [kRQ] ring
+        owner = rayq + kRQ;                  // uint [64] round-stamped claims, indexed by pair slot
+        pdat = owner + 64;                   // [64][16] pair table: A[9], u0[3], w, rho, sigma, -
+        wave_stride = al4(pdat + 64 * 16);
         red = wave_base;                     // final reduction reuses the wave regions
         total = wave_base + kWaves * wave_stride;
         const int need_red = wave_base + kWaves * 64 * 29;
@@ -602,174 +581,43 @@ struct BwdLayout {
     }
 };
 
-// lane = chunk (<= kChunk bins of one ray) run serially; results (linear in the chunk's sums) are
-// grouped by pair with a ballot match and added to the pair accumulators by one leader per pair.
-template <int MODE, bool RAYS>
-__device__ __forceinline__ void bwd_chunks(const uint2* chq, int cnt, const float* pdat, const float* grow,
-                                           const float2* tth, const float2* tph, float* pacc, float* rows,
-                                           const float* gray, int np_, int nr, float r0, float dr, float inv_dr,
-                                           float cdt, float f0log2, float rscale) {
-    const int lane = lane_id();
-    const bool act = lane < cnt;
-    int slot = 64 + lane;   // inactive lanes get unique dummy keys
-    if (act) {
-        const uint2 e = chq[lane];
-        slot = e.x & 0xFF;
-        const int i = (e.x >> 8) & 0xFFF, j = e.x >> 20;
-        const int kl = e.y & 0xFFFF, kh = e.y >> 16;
-        PairLite q;
-        load_pair(pdat, slot, q);
-        const float2 th = tth[i], ph = tph[j];
-        const float dx = th.x * ph.x, dy = th.x * ph.y, dz = th.y;
-        Ray R;
-        ray_setup<true>(q.A, q.u0, dx, dy, dz, 0.f, r0, inv_dr, nr, R);
-        const float sti = th.x;
-        const float* grw = RAYS && gray ? gray + (size_t)(i * np_ + j) * nr : nullptr;
-        // centred bin coordinate kap = k - ks: pdf = exp2(c0 + c2 kap^2), dl = kap dr
-        const float c0 = -kHalfLog2e * R.m2min;
-        const float c2 = -kHalfLog2e * R.a * dr * dr;
-        float S0 = 0.f, S1 = 0.f, S2 = 0.f, dsig = 0.f, drho = 0.f;  // S_n = sum (dL/dpdf) pdf kap^n
-        if (MODE == NLOSGR_MODE_NOOCL) {
-            float kap = (float)kl - R.ks;
-            const bool rg = RAYS && grw;
-            for (int kk = kl; kk <= kh; ++kk, kap += 1.0f) {
-                const float pdf = fast_exp2(fmaf(c2, kap * kap, c0));
-                const float H = rg ? fmaf(grow[kk], sti, grw[kk] * rscale) : grow[kk];
-                const float hp = H * pdf;
-                const float t1 = hp * kap;
-                S0 += hp; S1 += t1; S2 = fmaf(t1, kap, S2);
-            }
-            if (!rg) { S0 *= sti; S1 *= sti; S2 *= sti; }
-            dsig = S0 * q.rho;
-            drho = S0 * q.sigma;
-            S0 *= q.w; S1 *= q.w; S2 *= q.w;
-        } else {
-            // netf (whole ray per chunk): dL/dD_j = c rho H_j T_j + (sum_{k>j} H_k out_k) f'_j / f_j
-            const float T0 = fast_exp2((float)kl * f0log2);
-            float T = T0, Etot = 0.f;
-            float kap = (float)kl - R.ks;
-            for (int kk = kl; kk <= kh; ++kk, kap += 1.0f) {
-                const float pdf = fast_exp2(fmaf(c2, kap * kap, c0));
-                const float D = q.sigma * pdf;
-                float H = grow[kk] * sti;
-                if (RAYS && grw) H += grw[kk] * rscale;
-                Etot += H * cdt * q.rho * D * T;
-                T *= (__expf(-D * cdt) + 1e-7f);
-            }
-            T = T0;
-            float pre = 0.f;
-            kap = (float)kl - R.ks;
-            for (int kk = kl; kk <= kh; ++kk, kap += 1.0f) {
-                const float pdf = fast_exp2(fmaf(c2, kap * kap, c0));
-                const float D = q.sigma * pdf;
-                float H = grow[kk] * sti;
-                if (RAYS && grw) H += grw[kk] * rscale;
-                const float ee = __expf(-D * cdt);
-                const float f = ee + 1e-7f;
-                pre += H * cdt * q.rho * D * T;
-                const float dD = cdt * q.rho * H * T + (Etot - pre) * (-cdt * ee) * frcp(f);
-                drho += H * cdt * D * T;
-                dsig += dD * pdf;
-                const float hp = dD * q.sigma * pdf;
-                const float t1 = hp * kap;
-                S0 += hp; S1 += t1; S2 = fmaf(t1, kap, S2);
-                T *= f;
-            }
-        }
-        S1 *= dr;
-        S2 *= dr * dr;
-        // pdf = exp(-|z|^2/2), z = z* + dl v  ->  dL/du0 = -sum P z,  dL/dv = -sum P r z,  dA += dV (x) d
-        float zv[3], dV[3];
-        for (int r = 0; r < 3; ++r) {
-            zv[r] = S0 * R.zs[r] + S1 * R.v[r];
-            dV[r] = -(R.ts * zv[r] + S1 * R.zs[r] + S2 * R.v[r]);
-        }
-        float4* row = reinterpret_cast<float4*>(rows + lane * 16);
-        row[0] = make_float4(-zv[0], -zv[1], -zv[2], dV[0] * dx);
-        row[1] = make_float4(dV[0] * dy, dV[0] * dz, dV[1] * dx, dV[1] * dy);
-        row[2] = make_float4(dV[1] * dz, dV[2] * dx, dV[2] * dy, dV[2] * dz);
-        row[3] = make_float4(dsig, drho, 0.f, 0.f);
-    }
-    // group lanes by pair slot (7-bit keys) and let the lowest lane of each group reduce it
-    unsigned long long peers = ~0ull;
-#pragma unroll
-    for (int b = 0; b < 7; ++b) {
-        const bool bit = (slot >> b) & 1;
-        const unsigned long long m = __builtin_amdgcn_ballot_w64(bit);
-        peers &= bit ? m : ~m;
-    }
-    wave_sync();
-    const bool leader = act && (lanes_below(peers) == 0);
-    if (leader) {
-        float s[16];
-#pragma unroll
-        for (int t = 0; t < 16; ++t) s[t] = 0.f;
-        unsigned long long pm = peers;
-        while (pm) {
-            const int l = __builtin_ctzll(pm);
-            pm &= pm - 1;
-            const float4* row = reinterpret_cast<const float4*>(rows + l * 16);
-#pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                const float4 v = row[t];
-                s[4 * t] += v.x; s[4 * t + 1] += v.y; s[4 * t + 2] += v.z; s[4 * t + 3] += v.w;
-            }
-        }
-        float4* pa = reinterpret_cast<float4*>(pacc + slot * 16);
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            float4 v = pa[t];
-            v.x += s[4 * t]; v.y += s[4 * t + 1]; v.z += s[4 * t + 2]; v.w += s[4 * t + 3];
-            pa[t] = v;
-        }
-    }
-    wave_sync();
-}
+// per-lane backward segment state
+struct BRay {
+    int pos, rem, slot, ij, kl, len;
+    float kap, kap0, c0, c2, st;
+    float S0, S1, S2;
+    float zs[3], v[3], ts;
+    float w, rho, sigma;
+    float T, T0, Etot, pre, dsig, drho;  // netf
+    bool ph1;                            // netf: second pass
+};
 
-// lane = ray-queue entry: exact support test, then its chunks are appended to the chunk queue
-// (drained 64 at a time).
-template <int MODE, bool DENSE, bool RAYS>
-__device__ __forceinline__ void bwd_rays(const unsigned* rayq, int cnt, uint2* chq, int& ccnt, const float* pdat,
-                                         const float* grow, const float2* tth, const float2* tph, float* pacc,
-                                         float* rows, const float* gray, int np_, int nr, float mc2, float r0,
-                                         float dr, float inv_dr, float cdt, float f0log2, float rscale) {
-    const int lane = lane_id();
-    int ckl = 1, ckh = 0, step = 1;
-    unsigned cid = 0;
-    if (lane < cnt) {
-        cid = rayq[lane];
-        const int slot = cid & 0xFF, i = (cid >> 8) & 0xFFF, j = cid >> 20;
-        PairLite q;
-        load_pair(pdat, slot, q);
-        const float2 th = tth[i], ph = tph[j];
-        Ray R;
-        if (ray_setup<DENSE>(q.A, q.u0, th.x * ph.x, th.x * ph.y, th.y, mc2, r0, inv_dr, nr, R)) {
-            ckl = R.kl; ckh = R.kh;
-            const int len = R.kh - R.kl + 1;
-            const int nch = (len + kChunk - 1) / kChunk;
-            step = MODE == NLOSGR_MODE_NETF ? len : (len + nch - 1) / nch;
-        }
+template <int MODE, bool DENSE>
+__device__ __forceinline__ bool bray_setup(const float* pd, float2 th, float2 ph, int slot, int i, int j, int nr,
+                                           float mc2, float r0, float dr, float inv_dr, float f0log2, BRay& b) {
+    const float4* q4 = reinterpret_cast<const float4*>(pd);
+    const float4 a = q4[0], c = q4[1], e = q4[2], g = q4[3];
+    const float A[9] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w, e.x};
+    const float u0[3] = {e.y, e.z, e.w};
+    Ray R;
+    if (!ray_setup<DENSE>(A, u0, th.x * ph.x, th.x * ph.y, th.y, mc2, r0, inv_dr, nr, R)) return false;
+    b.pos = R.kl; b.kl = R.kl;
+    b.len = b.rem = R.kh - R.kl + 1;
+    b.slot = slot; b.ij = i | (j << 16);
+    b.kap = b.kap0 = (float)R.kl - R.ks;
+    b.c0 = -kHalfLog2e * R.m2min;
+    b.c2 = -kHalfLog2e * R.a * dr * dr;
+    b.st = th.x;
+    b.S0 = b.S1 = b.S2 = 0.f;
+    for (int r = 0; r < 3; ++r) { b.zs[r] = R.zs[r]; b.v[r] = R.v[r]; }
+    b.ts = R.ts;
+    b.w = g.x; b.rho = g.y; b.sigma = g.z;
+    if (MODE == NLOSGR_MODE_NETF) {
+        b.T = b.T0 = fast_exp2((float)R.kl * f0log2);
+        b.Etot = b.pre = b.dsig = b.drho = 0.f;
+        b.ph1 = false;
     }
-    while (__builtin_amdgcn_ballot_w64(ckl <= ckh)) {
-        const bool pass = ckl <= ckh;
-        uint2 e;
-        if (pass) {
-            const int ce = min(ckh, ckl + step - 1);
-            e = make_uint2(cid, (unsigned)ckl | ((unsigned)ce << 16));
-            ckl = ce + 1;
-        }
-        const unsigned long long m = __builtin_amdgcn_ballot_w64(pass);
-        if (pass) chq[ccnt + lanes_below(m)] = e;
-        ccnt += __popcll(m);
-        if (ccnt >= 64) {
-            wave_sync();
-            bwd_chunks<MODE, RAYS>(chq, 64, pdat, grow, tth, tph, pacc, rows, gray, np_, nr, r0, dr, inv_dr, cdt,
-                                   f0log2, rscale);
-            if (lane < ccnt - 64) chq[lane] = chq[64 + lane];
-            wave_sync();
-            ccnt -= 64;
-        }
-    }
+    return true;
 }
 
 template <int PRESET, int MODE, bool DENSE, bool RAYS>
@@ -777,26 +625,18 @@ __global__ __launch_bounds__(kBlock) void bwd_kernel(KArgs k) {
     extern __shared__ __align__(16) float smem[];
     const int nr = k.geo.nr, nt = k.geo.nt, np_ = k.geo.np, P_ = k.geo.nwall;
     const BwdLayout L(nr, nt, np_);
-    GaussRec* srec = reinterpret_cast<GaussRec*>(smem + L.recs);
     const int wave = threadIdx.x >> 6, lane = lane_id();
     float* wb = smem + L.wave_base + wave * L.wave_stride;
     float* grow = wb + L.grow;
     float2* tth = reinterpret_cast<float2*>(wb + L.tth);
     float2* tph = reinterpret_cast<float2*>(wb + L.tph);
-    float* pdat = wb + L.pdat;
-    float* pacc = wb + L.pacc;
-    float* rows = wb + L.rows;
     unsigned* rayq = reinterpret_cast<unsigned*>(wb + L.rayq);
-    uint2* chq = reinterpret_cast<uint2*>(wb + L.chq);
+    unsigned* owner = reinterpret_cast<unsigned*>(wb + L.owner);
+    float* pdat = wb + L.pdat;
 
     const int gb = blockIdx.x * kNB;
     const int gi = gb + lane;
     const bool active = gi < k.g.ng;
-    for (int t = threadIdx.x; t < kNB; t += blockDim.x)
-        if (gb + t < k.g.ng) srec[t] = k.recs[gb + t];
-    for (int t = lane; t < 64 * 16; t += 64) pacc[t] = 0.f;
-    __syncthreads();
-
     const int split = blockIdx.y;
     const int per = (P_ + k.nsplit - 1) / k.nsplit;
     const int pbeg = split * per, pend = min(P_, pbeg + per);
@@ -816,78 +656,229 @@ __global__ __launch_bounds__(kBlock) void bwd_kernel(KArgs k) {
     dMu[0] = dMu[1] = dMu[2] = 0.f;
 #pragma unroll
     for (int t = 0; t < kMaxK; ++t) dF[t] = 0.f;
-    Pair P;
     float mu[3] = {0.f, 0.f, 0.f};
-    P.i0 = P.i1 = P.j0 = P.j1 = 0;
-    if (active) load_rec(srec[lane], P, mu);
+    if (active) {
+        const GaussRec rec = k.recs[gi];
+        mu[0] = rec.a.x; mu[1] = rec.a.y; mu[2] = rec.a.z;
+    }
 
     for (int p = pbeg + wave; p < pend; p += kWaves) {
         // stage this wall point's upstream gradient row and tables (wave-private)
         const float hs = k.geo.hscale[p];
-        for (int t = lane; t < nr; t += 64) {
-            const float g = k.grad_hist ? k.grad_hist[(size_t)p * nr + t] : 0.f;
-            grow[t] = g * k.geo.att[t] * hs;
+        wave_sync();
+        for (int t = lane; t < nr + kBSteps; t += 64) {
+            const float g = (k.grad_hist && t < nr) ? k.grad_hist[(size_t)p * nr + t] : 0.f;
+            grow[t] = t < nr ? g * k.geo.att[t] * hs : 0.f;
         }
         for (int t = lane; t < nt; t += 64)
             tth[t] = make_float2(k.geo.sin_theta[(size_t)p * nt + t], k.geo.cos_theta[(size_t)p * nt + t]);
         for (int t = lane; t < np_; t += 64)
             tph[t] = make_float2(k.geo.cos_phi[(size_t)p * np_ + t], k.geo.sin_phi[(size_t)p * np_ + t]);
+        owner[lane] = 0xFFFFFFFFu;
         const float px = k.geo.wall[3 * p], py = k.geo.wall[3 * p + 1], pz = k.geo.wall[3 * p + 2];
+        // pair setup (lane = Gaussian gi at wall point p); the ray pass reads the pair table
         bool more = false;
+        float M[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        int i0 = 0, i1 = -1, j0 = 0, j1 = -1;
+        float wpair = 0.f;
         if (active) {
+            Pair P;
+            float mu_[3];
+            load_rec(k.recs[gi], P, mu_);
             pair_setup<PRESET, DENSE>(k, gi, mu, px, py, pz, k.geo.grid_lin + 4 * (size_t)p, mc2, P);
             more = (P.w > 0.f) && P.i0 <= P.i1 && P.j0 <= P.j1;
-            store_pair(pdat, lane, P, 0.f);
+            for (int t = 0; t < 6; ++t) M[t] = P.M[t];
+            i0 = P.i0; i1 = P.i1; j0 = P.j0; j1 = P.j1;
+            wpair = P.w;
+            float4* d4 = reinterpret_cast<float4*>(pdat + lane * 16);
+            d4[0] = make_float4(P.A[0], P.A[1], P.A[2], P.A[3]);
+            d4[1] = make_float4(P.A[4], P.A[5], P.A[6], P.A[7]);
+            d4[2] = make_float4(P.A[8], P.u0[0], P.u0[1], P.u0[2]);
+            d4[3] = make_float4(P.w, P.rho, P.sigma, 0.f);
         }
         const float* gray = RAYS && k.grad_ray ? k.grad_ray + (size_t)p * nt * np_ * nr : nullptr;
         wave_sync();
-        int ci = P.i0, cj = P.j0, cnt = 0, ccnt = 0;
+        int ci = i0, cj = j0, qhead = 0, qcount = 0;
+        unsigned round = 0;
+        bool act = false, pend = false;
+        float dU0p[3] = {0.f, 0.f, 0.f}, drho_pair = 0.f;
+        BRay b;
+        b.pos = 0; b.rem = 0; b.slot = lane; b.ij = 0; b.kl = 0; b.len = 0;
+        b.kap = b.kap0 = b.c0 = b.c2 = b.st = 0.f;
+        b.S0 = b.S1 = b.S2 = 0.f;
+        b.zs[0] = b.zs[1] = b.zs[2] = b.v[0] = b.v[1] = b.v[2] = b.ts = 0.f;
+        b.w = b.rho = b.sigma = 0.f;
+        b.T = b.T0 = b.Etot = b.pre = b.dsig = b.drho = 0.f;
+        b.ph1 = false;
+        // pending result of a finished ray: dL/du0, dL/dv, dsigma, drho
+        float rU[3] = {0.f, 0.f, 0.f}, rV[3] = {0.f, 0.f, 0.f}, rSig = 0.f, rRho = 0.f;
         while (true) {
-            enumerate<DENSE>(P, more, ci, cj, tth, tph, rayq, cnt);
-            if (cnt == 0) break;
-            wave_sync();
-            const int nb = min(cnt, 64);
-            bwd_rays<MODE, DENSE, RAYS>(rayq, nb, chq, ccnt, pdat, grow, tth, tph, pacc, rows, gray, np_, nr, mc2, r0,
-                                        dr, inv_dr, cdt, f0log2, rscale);
-            wave_sync();
-            if (lane < cnt - nb) rayq[lane] = rayq[nb + lane];
-            wave_sync();
-            cnt -= nb;
-        }
-        if (ccnt > 0) {
-            wave_sync();
-            bwd_chunks<MODE, RAYS>(chq, ccnt, pdat, grow, tth, tph, pacc, rows, gray, np_, nr, r0, dr, inv_dr, cdt,
-                                   f0log2, rscale);
-        }
-        wave_sync();
-        // per-pair chain for this wave's pair (Gaussian gi, wall point p)
-        if (active) {
-            float* pa = pacc + lane * 16;
-            const float dU0[3] = {pa[0], pa[1], pa[2]};
-            for (int r = 0; r < 3; ++r) {  // u0 = A (p - mu)
-                dA[3 * r] += pa[3 + 3 * r] + dU0[r] * P.q[0];
-                dA[3 * r + 1] += pa[4 + 3 * r] + dU0[r] * P.q[1];
-                dA[3 * r + 2] += pa[5 + 3 * r] + dU0[r] * P.q[2];
+            if (qcount < 64 && __builtin_amdgcn_ballot_w64(more)) {
+                wave_sync();
+                enumerate_box<DENSE>(M, i1, j0, j1, more, ci, cj, tth, tph, rayq, qhead, qcount);
+                wave_sync();
             }
-            for (int c = 0; c < 3; ++c) dMu[c] -= P.A[c] * dU0[0] + P.A[3 + c] * dU0[1] + P.A[6 + c] * dU0[2];
-            dSig += pa[12];
-            const float drho = pa[13];
-            for (int t = 0; t < 16; ++t) pa[t] = 0.f;
-            // rho = max(0, 0.5 + sum_c f_c Y_c(dir)); torch's clamp_min passes the gradient at equality
-            if (P.w > 0.f && P.sh + 0.5f >= 0.f && drho != 0.f) {
-                float Y[kMaxK];
-                sh_basis<PRESET>(deg, P.dir[0], P.dir[1], P.dir[2], Y);
+            const bool anymore = __builtin_amdgcn_ballot_w64(more) != 0;
+            const unsigned long long idle = __builtin_amdgcn_ballot_w64(!act && !pend);
+            const int nidle = __popcll(idle);
+            if (qcount > 0 && (nidle >= kRefill || !anymore)) {
+                const int r = lanes_below(idle);
+                const bool take = !act && !pend && r < qcount;
+                if (take) {
+                    const unsigned e = rayq[(qhead + r) & (kRQ - 1)];
+                    const int slot = e & 0xFF, i = (e >> 8) & 0xFFF, j = e >> 20;
+                    act = bray_setup<MODE, DENSE>(pdat + slot * 16, tth[i], tph[j], slot, i, j, nr, mc2, r0, dr,
+                                                  inv_dr, f0log2, b);
+                }
+                const int ntake = min(nidle, qcount);
+                qhead = (qhead + ntake) & (kRQ - 1);
+                qcount -= ntake;
+            }
+            const bool anyact = __builtin_amdgcn_ballot_w64(act) != 0;
+            const bool anypend = __builtin_amdgcn_ballot_w64(pend) != 0;
+            if (!anyact && !anypend) {
+                if (!anymore && qcount == 0) break;
+                continue;
+            }
+            if (anyact) {
+                const int remw = act ? b.rem : 0;
+                const float* gr = grow + (act ? b.pos : 0);
+                const float* gw = RAYS && gray ? gray + (size_t)((b.ij & 0xFFFF) * np_ + (b.ij >> 16)) * nr + b.pos
+                                               : nullptr;
+                float Hs[kBSteps];
 #pragma unroll
-                for (int c = 0; c < kMaxK; ++c)
-                    if (c < K) dF[c] += drho * Y[c];
+                for (int m = 0; m < kBSteps; ++m) {
+                    float H = gr[m];
+                    if (RAYS || MODE == NLOSGR_MODE_NETF) H *= b.st;
+                    if (RAYS && gw && m < remw) H += gw[m] * rscale;
+                    Hs[m] = m < remw ? H : 0.f;
+                }
+                float kap = b.kap;
+                if (MODE == NLOSGR_MODE_NOOCL) {
+                    float S0 = b.S0, S1 = b.S1, S2 = b.S2;
+#pragma unroll
+                    for (int m = 0; m < kBSteps; ++m) {
+                        const float hp = Hs[m] * fast_exp2(fmaf(b.c2, kap * kap, b.c0));
+                        const float t1 = hp * kap;
+                        S0 += hp; S1 += t1; S2 = fmaf(t1, kap, S2);
+                        kap += 1.f;
+                    }
+                    b.S0 = S0; b.S1 = S1; b.S2 = S2;
+                } else {
+                    // dL/dD_j = c rho H_j T_j + (sum_{k>j} H_k out_k) f'_j / f_j  (two passes per ray)
+                    float T = b.T, Etot = b.Etot, pre = b.pre;
+                    float S0 = b.S0, S1 = b.S1, S2 = b.S2, dsig = b.dsig, drho = b.drho;
+#pragma unroll
+                    for (int m = 0; m < kBSteps; ++m) {
+                        const bool in = m < remw;
+                        const float pdf = fast_exp2(fmaf(b.c2, kap * kap, b.c0));
+                        const float D = b.sigma * pdf;
+                        const float H = Hs[m];
+                        const float ee = __expf(-D * cdt);
+                        const float f = ee + 1e-7f;
+                        const float term = H * cdt * b.rho * D * T;
+                        if (!b.ph1) {
+                            Etot += term;
+                        } else {
+                            pre += term;
+                            const float dD = in ? cdt * b.rho * H * T + (Etot - pre) * (-cdt * ee) * frcp(f) : 0.f;
+                            drho += H * cdt * D * T;
+                            const float hp = dD * b.sigma * pdf;
+                            dsig += dD * pdf;
+                            const float t1 = hp * kap;
+                            S0 += hp; S1 += t1; S2 = fmaf(t1, kap, S2);
+                        }
+                        T *= in ? f : 1.f;
+                        kap += 1.f;
+                    }
+                    b.T = T; b.Etot = Etot; b.pre = pre;
+                    b.S0 = S0; b.S1 = S1; b.S2 = S2; b.dsig = dsig; b.drho = drho;
+                }
+                if (act) {
+                    b.kap = kap;
+                    b.pos += kBSteps;
+                    b.rem -= kBSteps;
+                    if (MODE == NLOSGR_MODE_NETF && b.rem <= 0 && !b.ph1) {   // second pass from the start
+                        b.ph1 = true;
+                        b.pos = b.kl; b.rem = b.len; b.kap = b.kap0; b.T = b.T0;
+                    }
+                    if (b.rem <= 0) {
+                        // pdf = exp(-|z|^2/2), z = z* + dl v:  dL/du0 = -sum P z,  dL/dv = -sum P dl z
+                        float S0 = b.S0, S1 = b.S1 * dr, S2 = b.S2 * dr * dr;
+                        if (MODE == NLOSGR_MODE_NOOCL) {
+                            if (!RAYS) { S0 *= b.st; S1 *= b.st; S2 *= b.st; }
+                            rSig = S0 * b.rho;
+                            rRho = S0 * b.sigma;
+                            S0 *= b.w; S1 *= b.w; S2 *= b.w;
+                        } else {
+                            rSig = b.dsig;
+                            rRho = b.drho;
+                        }
+                        for (int r = 0; r < 3; ++r) {
+                            const float zv = S0 * b.zs[r] + S1 * b.v[r];
+                            rU[r] = -zv;
+                            rV[r] = -(b.ts * zv + S1 * b.zs[r] + S2 * b.v[r]);
+                        }
+                        act = false;
+                        pend = true;
+                    }
+                }
+            }
+            if (__builtin_amdgcn_ballot_w64(pend)) {
+                // hand finished rays to their pair lanes (one claimant per pair per round)
+                const unsigned stamp = (round << 8) | (unsigned)lane;
+                if (pend) owner[b.slot] = stamp;
+                wave_sync();
+                const unsigned o = owner[lane];
+                const bool got = (o >> 8) == (round & 0xFFFFFFu);
+                const bool won = pend && owner[b.slot] == stamp;
+                const int src = got ? (int)(o & 63u) : lane;
+                const float gm = got ? 1.f : 0.f;
+                float gU[3], gV[3];
+#pragma unroll
+                for (int c = 0; c < 3; ++c) { gU[c] = gm * __shfl(rU[c], src); gV[c] = gm * __shfl(rV[c], src); }
+                const float gSig = gm * __shfl(rSig, src), gRho = gm * __shfl(rRho, src);
+                // every lane must execute the bpermute: it cannot read lanes that are inactive in EXEC
+                const int sij = __shfl(b.ij, src);
+                const int gij = got ? sij : 0;
+                const float2 th = tth[gij & 0xFFFF], ph = tph[gij >> 16];
+                const float d3[3] = {th.x * ph.x, th.x * ph.y, th.y};
+                for (int r = 0; r < 3; ++r)
+                    for (int c = 0; c < 3; ++c) dA[3 * r + c] += gV[r] * d3[c];
+                for (int r = 0; r < 3; ++r) dU0p[r] += gU[r];
+                dSig += gSig;
+                drho_pair += gRho;
+                wave_sync();
+                if (won) pend = false;
+                ++round;
+            }
+        }
+        // chain of this wall point's pair (Gaussian gi, wall point p): u0 = A (p - mu) and the
+        // SH view direction.  rho = max(0, 0.5 + sum_c f_c Y_c(dir)); w > 0 implies rho > 0.
+        if (active && wpair > 0.f) {
+            const float q[3] = {px - mu[0], py - mu[1], pz - mu[2]};
+            const float4* d4 = reinterpret_cast<const float4*>(pdat + lane * 16);
+            const float4 a = d4[0], c = d4[1], e = d4[2];
+            const float A[9] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w, e.x};
+            for (int r = 0; r < 3; ++r)
+                for (int cc = 0; cc < 3; ++cc) dA[3 * r + cc] += dU0p[r] * q[cc];
+            for (int cc = 0; cc < 3; ++cc) dMu[cc] -= A[cc] * dU0p[0] + A[3 + cc] * dU0p[1] + A[6 + cc] * dU0p[2];
+            if (drho_pair != 0.f) {
+                float dir[3], nrm;
+                view_dir<PRESET>(-q[0], -q[1], -q[2], dir[0], dir[1], dir[2], nrm);
+                float Y[kMaxK];
+                sh_basis<PRESET>(deg, dir[0], dir[1], dir[2], Y);
+#pragma unroll
+                for (int cc = 0; cc < kMaxK; ++cc)
+                    if (cc < K) dF[cc] += drho_pair * Y[cc];
                 float gx, gy, gz;
-                sh_grad_dir<PRESET>(deg, P.dir[0], P.dir[1], P.dir[2], fg, gx, gy, gz);
+                sh_grad_dir<PRESET>(deg, dir[0], dir[1], dir[2], fg, gx, gy, gz);
                 float ox, oy, oz;
-                view_dir_bwd<PRESET>(-P.q[0], -P.q[1], -P.q[2], P.nrm, drho * gx, drho * gy, drho * gz, ox, oy, oz);
+                view_dir_bwd<PRESET>(-q[0], -q[1], -q[2], nrm, drho_pair * gx, drho_pair * gy, drho_pair * gz, ox,
+                                     oy, oz);
                 dMu[0] += ox; dMu[1] += oy; dMu[2] += oz;
             }
         }
-        wave_sync();
     }
     // fixed-order combination of the 4 waves' accumulators -> partial slab
     __syncthreads();
