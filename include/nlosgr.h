@@ -24,6 +24,12 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#if defined(__GNUC__) || defined(__clang__)
+#define NLOSGR_API __attribute__((visibility("default")))
+#else
+#define NLOSGR_API
+#endif
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -92,7 +98,7 @@ typedef struct {
 } nlosgr_options;
 
 /* Scratch bytes needed by fwd/bwd for this problem (caller allocates, 256-B aligned). */
-size_t nlosgr_workspace_bytes(const nlosgr_gaussians* g, const nlosgr_geometry* geo,
+NLOSGR_API size_t nlosgr_workspace_bytes(const nlosgr_gaussians* g, const nlosgr_geometry* geo,
                               const nlosgr_options* opt);
 
 /* Forward.  hist_out [P,nr] (may be NULL):  hscale[p]*att[k]*sum_{g,i,j} w_g(p) sin(theta_i) pdf
@@ -100,14 +106,14 @@ size_t nlosgr_workspace_bytes(const nlosgr_gaussians* g, const nlosgr_geometry* 
  *           rays in the reference's (i,j) meshgrid('ij') order, samples contiguous — the layout of
  *           _C.render_rays' rho_density [N_rays, N_samples].
  * w_g(p) = sigmoid(opacity_g) * max(0, 0.5 + SH_g(dir(mu_g - wall_p))). */
-int nlosgr_render_fwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo,
+NLOSGR_API int nlosgr_render_fwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo,
                       const nlosgr_options* opt, void* workspace, float* hist_out,
                       float* ray_out, void* hip_stream);
 
 /* Backward.  grad_hist [P,nr] and/or grad_ray [P,nt*np,nr] (either may be NULL).
  * Writes (overwrites) the gradients of the RAW parameters: d_mu [ng,3], d_scaling [ng,3],
  * d_rotation [ng,4], d_opacity [ng], d_features [ng,k_feat]. */
-int nlosgr_render_bwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo,
+NLOSGR_API int nlosgr_render_bwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo,
                       const nlosgr_options* opt, void* workspace, const float* grad_hist,
                       const float* grad_ray, float* d_mu, float* d_scaling, float* d_rotation,
                       float* d_opacity, float* d_features, void* hip_stream);
@@ -115,16 +121,55 @@ int nlosgr_render_bwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo,
 /* Work count of one forward at opt->cutoff (no outputs written): counts (DEVICE, [3] uint64,
  * overwritten) = {in-support (wall point, Gaussian) pairs, in-support rays (pair, i, j),
  * in-support evaluations (pair, i, j, k)} — the unit of the VALU roofline. */
-int nlosgr_count_support(const nlosgr_gaussians* g, const nlosgr_geometry* geo,
+NLOSGR_API int nlosgr_count_support(const nlosgr_gaussians* g, const nlosgr_geometry* geo,
                          const nlosgr_options* opt, void* workspace, unsigned long long* counts,
                          void* hip_stream);
 
 /* 3-sigma (sigma_scale) axis-aligned boxes [ng,6] = (min xyz, max xyz) under the preset's scale
  * convention (bbox_compute.cuh:23-71 for "cuda"; gaussian_model.py:140-178 for "torch"). */
-int nlosgr_bboxes(const nlosgr_gaussians* g, float sigma_scale, float* bboxes_out, void* hip_stream);
+NLOSGR_API int nlosgr_bboxes(const nlosgr_gaussians* g, float sigma_scale, float* bboxes_out, void* hip_stream);
 
-const char* nlosgr_last_error(void);
-int nlosgr_abi_version(void);
+/* ---------------------------------------------------------------------------------------
+ * Path C "rays" API: arbitrary rays x = o + t d (cuda_autograd.py:18-191 -> _C.render_rays,
+ * volume_renderer.cu:189-305; _C.filter_gaussians_per_ray, ray_aabb.cu:63-102).
+ * ------------------------------------------------------------------------------------- */
+#define NLOSGR_MAX_PER_RAY 256   /* MAX_GAUSSIANS_PER_RAY, ray_aabb.cu:6 */
+
+typedef struct nlosgr_rays {
+    int32_t nrays;            /* N_rays */
+    int32_t nsamp;            /* N_samples (<= 8192) */
+    const float* origins;     /* [nrays,3] */
+    const float* dirs;        /* [nrays,3], used as given: x = o + t d */
+    const float* t;           /* [nsamp] */
+    const float* cam;         /* [3] camera position: SH view direction mu - cam */
+} nlosgr_rays;
+
+/* Scratch bytes for nlosgr_rays_fwd / nlosgr_rays_bwd. */
+NLOSGR_API size_t nlosgr_rays_workspace_bytes(const nlosgr_gaussians* g, const nlosgr_rays* r);
+
+/* filter_out [nrays, 1 + NLOSGR_MAX_PER_RAY] int32: count, then the first (by index) Gaussians
+ * whose box bboxes[g] = (min xyz, max xyz) the half-infinite ray hits (slab test with
+ * 1/(d + 1e-8), cuda_utils.cuh:97-121), -1 padding — the layout filter_gaussians_per_ray returns. */
+NLOSGR_API int nlosgr_filter_rays(const nlosgr_gaussians* g, const nlosgr_rays* r, const float* bboxes,
+                       int32_t* filter_out, void* hip_stream);
+
+/* Forward: rho_out, density_out, trans_out [nrays, nsamp] (volume_renderer.cu:16-185):
+ *   D = sum_{g in filter} sigmoid(o_g) pdf_g(x);  no occlusion: rho = c dT sum sigma pdf rho_g,
+ *   trans = 1;  occlusion: rho = T sum (1 - exp(-sigma pdf c dT)) rho_g, T_s = exp(-c dT
+ *   sum_{s'<s} D_s'), all three zero where T_s < 1e-4 (the reference's early exit). */
+NLOSGR_API int nlosgr_rays_fwd(const nlosgr_gaussians* g, const nlosgr_rays* r, const int32_t* filter,
+                    float c_deltaT, int32_t use_occlusion, void* workspace, float* rho_out,
+                    float* density_out, float* trans_out, void* hip_stream);
+
+/* Backward of nlosgr_rays_fwd w.r.t. the RAW parameters (the reference returns zeros,
+ * cuda_autograd.py:147-156).  Any of g_rho / g_density / g_trans may be NULL. */
+NLOSGR_API int nlosgr_rays_bwd(const nlosgr_gaussians* g, const nlosgr_rays* r, const int32_t* filter,
+                    float c_deltaT, int32_t use_occlusion, void* workspace, const float* g_rho,
+                    const float* g_density, const float* g_trans, float* d_mu, float* d_scaling,
+                    float* d_rotation, float* d_opacity, float* d_features, void* hip_stream);
+
+NLOSGR_API const char* nlosgr_last_error(void);
+NLOSGR_API int nlosgr_abi_version(void);
 
 #ifdef __cplusplus
 }

@@ -37,8 +37,11 @@ def build(force=False, save_temps=False, verbose=True):
     if not force and not needs_build():
         return OUT
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    # no SLP / loop vectorisation: packed-f32 VALU needs aligned register pairs, which raised the
+    # backward kernel's VGPR count past the 3-waves/SIMD limit (measured: bwd 736 -> 701 ms at C3)
     cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-munsafe-fp-atomics", "-I", os.path.join(ROOT, "include"), "-o", OUT + ".tmp"]
+           "-munsafe-fp-atomics", "-fno-slp-vectorize", "-fno-vectorize", "-fvisibility=hidden",
+           "-I", os.path.join(ROOT, "include"), "-o", OUT + ".tmp"]
     if save_temps:
         cmd += ["-save-temps"]
     cmd += sources()

@@ -1,0 +1,165 @@
+// Helpers shared by the translation units of libnlosgr (volume kernels, rays kernels):
+// error state of the C ABI, wave-level primitives, hardware fast math, the parameter
+// preprocessing kernel and the chain from dL/dA, dL/dsigma to the raw parameters.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "nlosgr_device.hpp"
+
+namespace nlosgr {
+namespace detail {
+
+inline thread_local char g_err[512] = "";
+
+inline int set_err(int code, const char* msg) {
+    snprintf(g_err, sizeof(g_err), "%s", msg);
+    return code;
+}
+
+constexpr int kBlock = 256;
+constexpr int kWaves = kBlock / 64;
+constexpr int kMaxK = 16;
+constexpr int kNB = 64;          // Gaussians per backward workgroup
+constexpr float kPi = 3.14159265358979323846f;
+constexpr float kHalfLog2e = 0.72134752044448170368f;  // log2(e)/2
+
+// float -> int index, saturated before the conversion (no UB for huge / non-finite values)
+__device__ __forceinline__ int fidx(float x, int lo, int hi) {
+    x = fminf(fmaxf(x, (float)lo), (float)hi);
+    return (int)x;
+}
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+
+__device__ __forceinline__ int lanes_below(unsigned long long mask) {
+    return __builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0));
+}
+
+// orders LDS traffic between lanes of one wave (no workgroup barrier needed)
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+}
+
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// ------------------------------------------------------------------------------------------
+// fast math (hardware v_rcp / v_sqrt / v_exp / v_log, ~1 ulp) and a polynomial atan2
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
+__device__ __forceinline__ float fsqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
+__device__ __forceinline__ float flog2(float x) { return __builtin_amdgcn_logf(x); }
+
+inline size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
+
+#define HIPCHK(x)                                                                  \
+    do {                                                                           \
+        hipError_t e_ = (x);                                                       \
+        if (e_ != hipSuccess) return set_err(NLOSGR_E_HIP, hipGetErrorString(e_)); \
+    } while (0)
+
+// ------------------------------------------------------------------------------------------
+// preprocess: raw params -> A = diag(1/s~) R', sigma, s_max, N = A^T A
+// ------------------------------------------------------------------------------------------
+template <int PRESET>
+__global__ __launch_bounds__(kBlock) void preprocess_kernel(nlosgr_gaussians g, GaussRec* recs) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= g.ng) return;
+    float S[3] = {g.scaling[3 * i], g.scaling[3 * i + 1], g.scaling[3 * i + 2]};
+    float Q[4] = {g.rotation[4 * i], g.rotation[4 * i + 1], g.rotation[4 * i + 2], g.rotation[4 * i + 3]};
+    GaussAct a;
+    activate<PRESET>(S, Q, g.opacity[i], g.scaling_modifier, a);
+    float A[9];
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) A[3 * r + c] = a.Rp[3 * r + c] / a.st[r];
+    float N[6];
+    const int ix[6][2] = {{0, 0}, {0, 1}, {0, 2}, {1, 1}, {1, 2}, {2, 2}};
+    for (int t = 0; t < 6; ++t) {
+        const int p = ix[t][0], q = ix[t][1];
+        N[t] = A[p] * A[q] + A[3 + p] * A[3 + q] + A[6 + p] * A[6 + q];
+    }
+    const float smax = fmaxf(a.st[0], fmaxf(a.st[1], a.st[2]));
+    GaussRec rec;
+    rec.a = make_float4(g.mu[3 * i], g.mu[3 * i + 1], g.mu[3 * i + 2], a.sigma);
+    rec.b = make_float4(A[0], A[1], A[2], A[3]);
+    rec.c = make_float4(A[4], A[5], A[6], A[7]);
+    rec.d = make_float4(A[8], smax, N[0], N[1]);
+    rec.e = make_float4(N[2], N[3], N[4], N[5]);
+    recs[i] = rec;
+}
+
+inline void launch_preprocess(const nlosgr_gaussians* g, GaussRec* recs, hipStream_t s) {
+    const int nb = (g->ng + kBlock - 1) / kBlock;
+    if (g->preset == NLOSGR_PRESET_TORCH)
+        hipLaunchKernelGGL(preprocess_kernel<NLOSGR_PRESET_TORCH>, dim3(nb), dim3(kBlock), 0, s, *g, recs);
+    else
+        hipLaunchKernelGGL(preprocess_kernel<NLOSGR_PRESET_CUDA>, dim3(nb), dim3(kBlock), 0, s, *g, recs);
+}
+
+// dL/dA (acc[0..8], A = diag(1/s~) R') -> dL/d_scaling, dL/d_rotation of Gaussian i under the preset
+template <int PRESET>
+__device__ void chain_to_raw(const nlosgr_gaussians& g, int i, const float* acc, float* d_scaling, float* d_rot) {
+    const float* S = g.scaling + 3 * i;
+    const float* Q = g.rotation + 4 * i;
+    const float O = g.opacity[i];
+    const float mod = g.scaling_modifier;
+    GaussAct a;
+    activate<PRESET>(S, Q, O, mod, a);
+    // A_rc = R'_rc / s~_r
+    float dRp[9], dst[3];
+    for (int r = 0; r < 3; ++r) {
+        float acc_s = 0.f;
+        for (int c = 0; c < 3; ++c) {
+            dRp[3 * r + c] = acc[3 * r + c] / a.st[r];
+            acc_s += acc[3 * r + c] * a.Rp[3 * r + c];
+        }
+        dst[r] = -acc_s / (a.st[r] * a.st[r]);
+    }
+    float dR[9];
+    if (PRESET == NLOSGR_PRESET_TORCH) {
+        for (int t = 0; t < 9; ++t) dR[t] = dRp[t];
+        for (int r = 0; r < 3; ++r) {
+            const float e = expf(S[r]) * mod;     // s = exp(e), ds/dS = s * e
+            d_scaling[3 * i + r] = dst[r] * a.st[r] * e;
+        }
+        // q^ = Q / max(|Q|,1e-12); qn = q^/|q^|; R = R(qn)
+        const float n0 = sqrtf(Q[0] * Q[0] + Q[1] * Q[1] + Q[2] * Q[2] + Q[3] * Q[3]);
+        const float d0 = fmaxf(n0, 1e-12f);
+        float qh[4] = {Q[0] / d0, Q[1] / d0, Q[2] / d0, Q[3] / d0};
+        const float n1 = sqrtf(qh[0] * qh[0] + qh[1] * qh[1] + qh[2] * qh[2] + qh[3] * qh[3]);
+        float qn[4] = {qh[0] / n1, qh[1] / n1, qh[2] / n1, qh[3] / n1};
+        float dqn[4];
+        quat_rot_bwd(qn[0], qn[1], qn[2], qn[3], dR, dqn[0], dqn[1], dqn[2], dqn[3]);
+        float dp = qn[0] * dqn[0] + qn[1] * dqn[1] + qn[2] * dqn[2] + qn[3] * dqn[3];
+        float dqh[4];
+        for (int t = 0; t < 4; ++t) dqh[t] = (dqn[t] - qn[t] * dp) / n1;
+        if (n0 > 1e-12f) {
+            float dp2 = qh[0] * dqh[0] + qh[1] * dqh[1] + qh[2] * dqh[2] + qh[3] * dqh[3];
+            for (int t = 0; t < 4; ++t) d_rot[4 * i + t] = (dqh[t] - qh[t] * dp2) / n0;
+        } else {
+            for (int t = 0; t < 4; ++t) d_rot[4 * i + t] = dqh[t] / d0;
+        }
+    } else {
+        // R' = R^T
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 3; ++c) dR[3 * c + r] = dRp[3 * r + c];
+        for (int r = 0; r < 3; ++r) d_scaling[3 * i + r] = dst[r] * (a.st[r] - 1e-8f);  // s = exp(S) mod
+        const float n = sqrtf(Q[0] * Q[0] + Q[1] * Q[1] + Q[2] * Q[2] + Q[3] * Q[3]);
+        if (n < 1e-8f) {
+            for (int t = 0; t < 4; ++t) d_rot[4 * i + t] = 0.f;
+        } else {
+            float qn[4] = {Q[0] / n, Q[1] / n, Q[2] / n, Q[3] / n};
+            float dqn[4];
+            quat_rot_bwd(qn[0], qn[1], qn[2], qn[3], dR, dqn[0], dqn[1], dqn[2], dqn[3]);
+            float dp = qn[0] * dqn[0] + qn[1] * dqn[1] + qn[2] * dqn[2] + qn[3] * dqn[3];
+            for (int t = 0; t < 4; ++t) d_rot[4 * i + t] = (dqn[t] - qn[t] * dp) / n;
+        }
+    }
+}
+
+}  // namespace detail
+}  // namespace nlosgr

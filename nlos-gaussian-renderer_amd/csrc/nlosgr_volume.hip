@@ -30,46 +30,12 @@
 #include <stdio.h>
 #include <string.h>
 
-#include "nlosgr_device.hpp"
+#include "nlosgr_common.hpp"
 
 using namespace nlosgr;
+using namespace nlosgr::detail;
 
 namespace {
-
-thread_local char g_err[512] = "";
-
-int set_err(int code, const char* msg) {
-    snprintf(g_err, sizeof(g_err), "%s", msg);
-    return code;
-}
-
-constexpr int kBlock = 256;
-constexpr int kWaves = kBlock / 64;
-constexpr int kMaxK = 16;
-constexpr int kNB = 64;          // Gaussians per backward workgroup
-constexpr float kPi = 3.14159265358979323846f;
-constexpr float kHalfLog2e = 0.72134752044448170368f;  // log2(e)/2
-
-// float -> int index, saturated before the conversion (no UB for huge / non-finite values)
-__device__ __forceinline__ int fidx(float x, int lo, int hi) {
-    x = fminf(fmaxf(x, (float)lo), (float)hi);
-    return (int)x;
-}
-
-__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
-
-__device__ __forceinline__ int lanes_below(unsigned long long mask) {
-    return __builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0));
-}
-
-// orders LDS traffic between lanes of one wave (no workgroup barrier needed)
-__device__ __forceinline__ void wave_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-}
-
-__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
 struct KArgs {
     nlosgr_gaussians g;
@@ -84,43 +50,6 @@ struct KArgs {
     int nsplit;
     unsigned long long* counts;  // optional [3]: pairs, segments, samples (nlosgr_count_support)
 };
-
-// ------------------------------------------------------------------------------------------
-// preprocess: raw params -> A = diag(1/s~) R', sigma, s_max, N = A^T A
-// ------------------------------------------------------------------------------------------
-template <int PRESET>
-__global__ __launch_bounds__(kBlock) void preprocess_kernel(nlosgr_gaussians g, GaussRec* recs) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= g.ng) return;
-    float S[3] = {g.scaling[3 * i], g.scaling[3 * i + 1], g.scaling[3 * i + 2]};
-    float Q[4] = {g.rotation[4 * i], g.rotation[4 * i + 1], g.rotation[4 * i + 2], g.rotation[4 * i + 3]};
-    GaussAct a;
-    activate<PRESET>(S, Q, g.opacity[i], g.scaling_modifier, a);
-    float A[9];
-    for (int r = 0; r < 3; ++r)
-        for (int c = 0; c < 3; ++c) A[3 * r + c] = a.Rp[3 * r + c] / a.st[r];
-    float N[6];
-    const int ix[6][2] = {{0, 0}, {0, 1}, {0, 2}, {1, 1}, {1, 2}, {2, 2}};
-    for (int t = 0; t < 6; ++t) {
-        const int p = ix[t][0], q = ix[t][1];
-        N[t] = A[p] * A[q] + A[3 + p] * A[3 + q] + A[6 + p] * A[6 + q];
-    }
-    const float smax = fmaxf(a.st[0], fmaxf(a.st[1], a.st[2]));
-    GaussRec rec;
-    rec.a = make_float4(g.mu[3 * i], g.mu[3 * i + 1], g.mu[3 * i + 2], a.sigma);
-    rec.b = make_float4(A[0], A[1], A[2], A[3]);
-    rec.c = make_float4(A[4], A[5], A[6], A[7]);
-    rec.d = make_float4(A[8], smax, N[0], N[1]);
-    rec.e = make_float4(N[2], N[3], N[4], N[5]);
-    recs[i] = rec;
-}
-
-// ------------------------------------------------------------------------------------------
-// fast math (hardware v_rcp / v_sqrt / v_exp / v_log, ~1 ulp) and a polynomial atan2
-// ------------------------------------------------------------------------------------------
-__device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
-__device__ __forceinline__ float fsqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
-__device__ __forceinline__ float flog2(float x) { return __builtin_amdgcn_logf(x); }
 
 // atan2 with |error| < 2e-6 rad (minimax on [0,1] + octant reduction); used only for the
 // conservative footprint box, which is widened by kAngMargin.
@@ -581,24 +510,29 @@ struct BwdLayout {
     }
 };
 
-// per-lane backward segment state
+// per-lane backward segment state (the ray geometry is recomputed from the pair table at finish)
 struct BRay {
     int pos, rem, slot, ij, kl, len;
     float kap, kap0, c0, c2, st;
     float S0, S1, S2;
-    float zs[3], v[3], ts;
-    float w, rho, sigma;
+    float rho, sigma;                    // netf
     float T, T0, Etot, pre, dsig, drho;  // netf
     bool ph1;                            // netf: second pass
 };
 
+__device__ __forceinline__ void load_pdat(const float* pd, float* A, float* u0, float& w, float& rho, float& sigma) {
+    const float4* q4 = reinterpret_cast<const float4*>(pd);
+    const float4 a = q4[0], c = q4[1], e = q4[2], g = q4[3];
+    A[0] = a.x; A[1] = a.y; A[2] = a.z; A[3] = a.w; A[4] = c.x; A[5] = c.y; A[6] = c.z; A[7] = c.w; A[8] = e.x;
+    u0[0] = e.y; u0[1] = e.z; u0[2] = e.w;
+    w = g.x; rho = g.y; sigma = g.z;
+}
+
 template <int MODE, bool DENSE>
 __device__ __forceinline__ bool bray_setup(const float* pd, float2 th, float2 ph, int slot, int i, int j, int nr,
                                            float mc2, float r0, float dr, float inv_dr, float f0log2, BRay& b) {
-    const float4* q4 = reinterpret_cast<const float4*>(pd);
-    const float4 a = q4[0], c = q4[1], e = q4[2], g = q4[3];
-    const float A[9] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w, e.x};
-    const float u0[3] = {e.y, e.z, e.w};
+    float A[9], u0[3], w, rho, sigma;
+    load_pdat(pd, A, u0, w, rho, sigma);
     Ray R;
     if (!ray_setup<DENSE>(A, u0, th.x * ph.x, th.x * ph.y, th.y, mc2, r0, inv_dr, nr, R)) return false;
     b.pos = R.kl; b.kl = R.kl;
@@ -609,10 +543,8 @@ __device__ __forceinline__ bool bray_setup(const float* pd, float2 th, float2 ph
     b.c2 = -kHalfLog2e * R.a * dr * dr;
     b.st = th.x;
     b.S0 = b.S1 = b.S2 = 0.f;
-    for (int r = 0; r < 3; ++r) { b.zs[r] = R.zs[r]; b.v[r] = R.v[r]; }
-    b.ts = R.ts;
-    b.w = g.x; b.rho = g.y; b.sigma = g.z;
     if (MODE == NLOSGR_MODE_NETF) {
+        b.rho = rho; b.sigma = sigma;
         b.T = b.T0 = fast_exp2((float)R.kl * f0log2);
         b.Etot = b.pre = b.dsig = b.drho = 0.f;
         b.ph1 = false;
@@ -706,8 +638,7 @@ __global__ __launch_bounds__(kBlock) void bwd_kernel(KArgs k) {
         b.pos = 0; b.rem = 0; b.slot = lane; b.ij = 0; b.kl = 0; b.len = 0;
         b.kap = b.kap0 = b.c0 = b.c2 = b.st = 0.f;
         b.S0 = b.S1 = b.S2 = 0.f;
-        b.zs[0] = b.zs[1] = b.zs[2] = b.v[0] = b.v[1] = b.v[2] = b.ts = 0.f;
-        b.w = b.rho = b.sigma = 0.f;
+        b.rho = b.sigma = 0.f;
         b.T = b.T0 = b.Etot = b.pre = b.dsig = b.drho = 0.f;
         b.ph1 = false;
         // pending result of a finished ray: dL/du0, dL/dv, dsigma, drho
@@ -804,20 +735,25 @@ __global__ __launch_bounds__(kBlock) void bwd_kernel(KArgs k) {
                     }
                     if (b.rem <= 0) {
                         // pdf = exp(-|z|^2/2), z = z* + dl v:  dL/du0 = -sum P z,  dL/dv = -sum P dl z
+                        float A[9], u0[3], w, rho, sigma;
+                        load_pdat(pdat + b.slot * 16, A, u0, w, rho, sigma);
+                        const float2 th = tth[b.ij & 0xFFFF], ph = tph[b.ij >> 16];
+                        Ray R;
+                        ray_setup<true>(A, u0, th.x * ph.x, th.x * ph.y, th.y, 0.f, r0, inv_dr, nr, R);
                         float S0 = b.S0, S1 = b.S1 * dr, S2 = b.S2 * dr * dr;
                         if (MODE == NLOSGR_MODE_NOOCL) {
                             if (!RAYS) { S0 *= b.st; S1 *= b.st; S2 *= b.st; }
-                            rSig = S0 * b.rho;
-                            rRho = S0 * b.sigma;
-                            S0 *= b.w; S1 *= b.w; S2 *= b.w;
+                            rSig = S0 * rho;
+                            rRho = S0 * sigma;
+                            S0 *= w; S1 *= w; S2 *= w;
                         } else {
                             rSig = b.dsig;
                             rRho = b.drho;
                         }
                         for (int r = 0; r < 3; ++r) {
-                            const float zv = S0 * b.zs[r] + S1 * b.v[r];
+                            const float zv = S0 * R.zs[r] + S1 * R.v[r];
                             rU[r] = -zv;
-                            rV[r] = -(b.ts * zv + S1 * b.zs[r] + S2 * b.v[r]);
+                            rV[r] = -(R.ts * zv + S1 * R.zs[r] + S2 * R.v[r]);
                         }
                         act = false;
                         pend = true;
@@ -915,64 +851,10 @@ __global__ __launch_bounds__(kBlock) void finish_kernel(KArgs k, float* d_mu, fl
         const float* src = k.partial + ((size_t)s * k.g.ng + i) * 32;
         for (int t = 0; t < 29; ++t) acc[t] += src[t];
     }
-    const float* S = k.g.scaling + 3 * i;
-    const float* Q = k.g.rotation + 4 * i;
-    const float O = k.g.opacity[i];
-    const float mod = k.g.scaling_modifier;
-    GaussAct a;
-    activate<PRESET>(S, Q, O, mod, a);
-    // A_rc = R'_rc / s~_r
-    float dRp[9], dst[3];
-    for (int r = 0; r < 3; ++r) {
-        float acc_s = 0.f;
-        for (int c = 0; c < 3; ++c) {
-            dRp[3 * r + c] = acc[3 * r + c] / a.st[r];
-            acc_s += acc[3 * r + c] * a.Rp[3 * r + c];
-        }
-        dst[r] = -acc_s / (a.st[r] * a.st[r]);
-    }
-    float dR[9];
-    if (PRESET == NLOSGR_PRESET_TORCH) {
-        for (int t = 0; t < 9; ++t) dR[t] = dRp[t];
-        for (int r = 0; r < 3; ++r) {
-            const float e = expf(S[r]) * mod;     // s = exp(e), ds/dS = s * e
-            d_scaling[3 * i + r] = dst[r] * a.st[r] * e;
-        }
-        // q^ = Q / max(|Q|,1e-12); qn = q^/|q^|; R = R(qn)
-        const float n0 = sqrtf(Q[0] * Q[0] + Q[1] * Q[1] + Q[2] * Q[2] + Q[3] * Q[3]);
-        const float d0 = fmaxf(n0, 1e-12f);
-        float qh[4] = {Q[0] / d0, Q[1] / d0, Q[2] / d0, Q[3] / d0};
-        const float n1 = sqrtf(qh[0] * qh[0] + qh[1] * qh[1] + qh[2] * qh[2] + qh[3] * qh[3]);
-        float qn[4] = {qh[0] / n1, qh[1] / n1, qh[2] / n1, qh[3] / n1};
-        float dqn[4];
-        quat_rot_bwd(qn[0], qn[1], qn[2], qn[3], dR, dqn[0], dqn[1], dqn[2], dqn[3]);
-        float dp = qn[0] * dqn[0] + qn[1] * dqn[1] + qn[2] * dqn[2] + qn[3] * dqn[3];
-        float dqh[4];
-        for (int t = 0; t < 4; ++t) dqh[t] = (dqn[t] - qn[t] * dp) / n1;
-        if (n0 > 1e-12f) {
-            float dp2 = qh[0] * dqh[0] + qh[1] * dqh[1] + qh[2] * dqh[2] + qh[3] * dqh[3];
-            for (int t = 0; t < 4; ++t) d_rot[4 * i + t] = (dqh[t] - qh[t] * dp2) / n0;
-        } else {
-            for (int t = 0; t < 4; ++t) d_rot[4 * i + t] = dqh[t] / d0;
-        }
-    } else {
-        // R' = R^T
-        for (int r = 0; r < 3; ++r)
-            for (int c = 0; c < 3; ++c) dR[3 * c + r] = dRp[3 * r + c];
-        for (int r = 0; r < 3; ++r) d_scaling[3 * i + r] = dst[r] * (a.st[r] - 1e-8f);  // s = exp(S) mod
-        const float n = sqrtf(Q[0] * Q[0] + Q[1] * Q[1] + Q[2] * Q[2] + Q[3] * Q[3]);
-        if (n < 1e-8f) {
-            for (int t = 0; t < 4; ++t) d_rot[4 * i + t] = 0.f;
-        } else {
-            float qn[4] = {Q[0] / n, Q[1] / n, Q[2] / n, Q[3] / n};
-            float dqn[4];
-            quat_rot_bwd(qn[0], qn[1], qn[2], qn[3], dR, dqn[0], dqn[1], dqn[2], dqn[3]);
-            float dp = qn[0] * dqn[0] + qn[1] * dqn[1] + qn[2] * dqn[2] + qn[3] * dqn[3];
-            for (int t = 0; t < 4; ++t) d_rot[4 * i + t] = (dqn[t] - qn[t] * dp) / n;
-        }
-    }
+    chain_to_raw<PRESET>(k.g, i, acc, d_scaling, d_rot);
     d_mu[3 * i] = acc[9]; d_mu[3 * i + 1] = acc[10]; d_mu[3 * i + 2] = acc[11];
-    d_opac[i] = acc[12] * a.sigma * (1.0f - a.sigma);
+    const float sg = 1.0f / (1.0f + expf(-k.g.opacity[i]));
+    d_opac[i] = acc[12] * sg * (1.0f - sg);
     const int kf = k.g.k_feat;
     const int K = (k.g.sh_degree + 1) * (k.g.sh_degree + 1);
 #pragma unroll
@@ -1016,7 +898,6 @@ __global__ __launch_bounds__(kBlock) void bbox_kernel(nlosgr_gaussians g, float 
 // ------------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------------
-size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
 
 int validate(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_options* opt) {
     if (!g || !geo || !opt) return set_err(NLOSGR_E_INVALID, "null argument struct");
@@ -1054,11 +935,6 @@ int bwd_nsplit(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlos
     return ns;
 }
 
-#define HIPCHK(x)                                                                  \
-    do {                                                                           \
-        hipError_t e_ = (x);                                                       \
-        if (e_ != hipSuccess) return set_err(NLOSGR_E_HIP, hipGetErrorString(e_)); \
-    } while (0)
 
 template <int PRESET, int MODE, bool DENSE, bool RAYS>
 void launch_fwd(const KArgs& ka, size_t shm, hipStream_t s) {
@@ -1091,13 +967,6 @@ void dispatch_bwd(const KArgs& ka, bool dense, bool rays, size_t shm, hipStream_
     }
 }
 
-void launch_preprocess(const nlosgr_gaussians* g, GaussRec* recs, hipStream_t s) {
-    const int nb = (g->ng + kBlock - 1) / kBlock;
-    if (g->preset == NLOSGR_PRESET_TORCH)
-        hipLaunchKernelGGL(preprocess_kernel<NLOSGR_PRESET_TORCH>, dim3(nb), dim3(kBlock), 0, s, *g, recs);
-    else
-        hipLaunchKernelGGL(preprocess_kernel<NLOSGR_PRESET_CUDA>, dim3(nb), dim3(kBlock), 0, s, *g, recs);
-}
 
 int run_fwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_options* opt, void* workspace,
             float* hist_out, float* ray_out, unsigned long long* counts, hipStream_t s) {

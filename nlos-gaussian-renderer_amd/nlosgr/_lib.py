@@ -9,7 +9,8 @@ import os
 import torch  # noqa: F401  (must precede the ctypes load: shared libamdhip64.so.7)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libnlosgr.so")
+# NLOSGR_LIB overrides the library path (A/B timing of alternative in-tree builds)
+LIB_PATH = os.environ.get("NLOSGR_LIB") or os.path.join(_HERE, "libnlosgr.so")
 
 PRESET_TORCH = 0
 PRESET_CUDA = 1
@@ -39,9 +40,17 @@ class Options(ctypes.Structure):
                 ("ray_scale", ctypes.c_float), ("nsplit", ctypes.c_int32), ("flags", ctypes.c_int32)]
 
 
+class Rays(ctypes.Structure):
+    _fields_ = [("nrays", ctypes.c_int32), ("nsamp", ctypes.c_int32), ("origins", _P), ("dirs", _P),
+                ("t", _P), ("cam", _P)]
+
+
+MAX_PER_RAY = 256   # NLOSGR_MAX_PER_RAY
+
 # every symbol include/nlosgr.h declares (tests check the exports against this list)
 EXPORTS = ["nlosgr_workspace_bytes", "nlosgr_render_fwd", "nlosgr_render_bwd", "nlosgr_count_support",
-           "nlosgr_bboxes", "nlosgr_last_error", "nlosgr_abi_version"]
+           "nlosgr_bboxes", "nlosgr_rays_workspace_bytes", "nlosgr_filter_rays", "nlosgr_rays_fwd",
+           "nlosgr_rays_bwd", "nlosgr_last_error", "nlosgr_abi_version"]
 
 _lib = None
 _load_error = None
@@ -65,6 +74,16 @@ def load():
     lib.nlosgr_render_bwd.restype = ctypes.c_int
     lib.nlosgr_count_support.argtypes = [PG, PGEO, POPT, _P, _P, _P]
     lib.nlosgr_count_support.restype = ctypes.c_int
+    PR = ctypes.POINTER(Rays)
+    lib.nlosgr_rays_workspace_bytes.argtypes = [PG, PR]
+    lib.nlosgr_rays_workspace_bytes.restype = ctypes.c_size_t
+    lib.nlosgr_filter_rays.argtypes = [PG, PR, _P, _P, _P]
+    lib.nlosgr_filter_rays.restype = ctypes.c_int
+    lib.nlosgr_rays_fwd.argtypes = [PG, PR, _P, ctypes.c_float, ctypes.c_int32, _P, _P, _P, _P, _P]
+    lib.nlosgr_rays_fwd.restype = ctypes.c_int
+    lib.nlosgr_rays_bwd.argtypes = [PG, PR, _P, ctypes.c_float, ctypes.c_int32, _P, _P, _P, _P, _P, _P, _P,
+                                    _P, _P, _P]
+    lib.nlosgr_rays_bwd.restype = ctypes.c_int
     lib.nlosgr_bboxes.argtypes = [PG, ctypes.c_float, _P, _P]
     lib.nlosgr_bboxes.restype = ctypes.c_int
     lib.nlosgr_last_error.argtypes = []

@@ -300,37 +300,65 @@ def mse_loss(hist, target):
 
 
 # --------------------------------------------------------------------------------------------
-# path C "rays" API: _C.render_rays (volume_renderer.cu:16-185, 189-305), dense (no AABB filter)
+# path C "rays" API: _C.filter_gaussians_per_ray + _C.render_rays (volume_renderer.cu:16-305)
 # --------------------------------------------------------------------------------------------
-def render_rays_cuda(ray_o, ray_d, t, P, sh_features, cam, deg, c, deltaT, mod, use_occlusion, mc=None):
-    """Per-(ray, sample) outputs [N_rays, N_samples] x3 with the cuda conventions.
+def bboxes_cuda(P, mod=1.0, sigma=3.0):
+    """bbox_compute.cuh:23-120 — [Ng, 6] (min xyz, max xyz); extent_i = sigma |R_i . s|, s = exp(S) mod
+    (no +1e-8 here), R from quat_to_rotmat (cuda_utils.cuh:54-85)."""
+    s = torch.exp(P._scaling) * mod
+    R = quat_to_rotmat_cuda(P._rotation)
+    ext = sigma * torch.sqrt(((R * s[:, None, :]) ** 2).sum(-1))
+    return torch.cat([P._mu - ext, P._mu + ext], dim=1)
 
-    No-occlusion branch volume_renderer.cu:138-183; occlusion branch :80-137 (shared T across
-    Gaussians, α = 1-exp(-σ pdf cΔT), early exit at T < 1e-4 zero-fills the rest)."""
+
+def aabb_filter(ray_o, ray_d, bboxes, cap=256):
+    """ray_aabb.cu:10-61 + cuda_utils.cuh:97-121 — int32 [N_rays, cap+1]: count, then the first
+    `cap` Gaussian indices (index order) whose box the half-infinite ray hits, -1 padding."""
+    inv = 1.0 / (ray_d + 1e-8)                                        # [R,3]
+    t0 = (bboxes[None, :, 0:3] - ray_o[:, None, :]) * inv[:, None, :]  # [R,Ng,3]
+    t1 = (bboxes[None, :, 3:6] - ray_o[:, None, :]) * inv[:, None, :]
+    tmin = torch.minimum(t0, t1).amax(-1)
+    tmax = torch.maximum(t0, t1).amin(-1)
+    hit = (tmax >= tmin) & (tmax >= 0)
+    out = torch.full((ray_o.shape[0], cap + 1), -1, dtype=torch.int32)
+    for r in range(ray_o.shape[0]):
+        idx = torch.nonzero(hit[r]).flatten()[:cap]
+        out[r, 0] = idx.numel()
+        out[r, 1:1 + idx.numel()] = idx.to(torch.int32)
+    return out
+
+
+def render_rays_cuda(ray_o, ray_d, t, P, sh_features, cam, deg, c, deltaT, mod, use_occlusion, filt=None,
+                     mc=None):
+    """Per-(ray, sample) outputs (rho_density, density, transmittance) [N_rays, N_samples].
+
+    volume_renderer.cu:16-185: each ray sums over the Gaussians of its filter row (all when
+    filt is None).  No occlusion (:138-183): rho = cΔT Σ σ pdf ρ, T = 1.  Occlusion (:80-137):
+    shared T across Gaussians, T_{s+1} = T_s exp(-D_s cΔT), rho = T Σ (1 - exp(-σ pdf cΔT)) ρ, and
+    after the first step with T_{s+1} < 1e-4 all three outputs are zero (early exit), i.e. a
+    sample is live iff T_s >= 1e-4."""
     nrays, nsamp = ray_o.shape[0], t.shape[0]
     x = (ray_o[:, None, :] + ray_d[:, None, :] * t[None, :, None]).reshape(-1, 3)
-    pdf = gaussian_pdf(x, P, "cuda", mod, mc)                       # [Ng, R*S]
-    sig = torch.sigmoid(P._opacity)                                  # [Ng,1]
+    pdf = gaussian_pdf(x, P, "cuda", mod, mc).view(-1, nrays, nsamp)   # [Ng, R, S]
+    if filt is not None:
+        mask = torch.zeros(P._mu.shape[0], nrays)
+        for r in range(nrays):
+            n = int(filt[r, 0])
+            if n > 0:
+                mask[filt[r, 1:1 + n].long(), r] = 1.0
+        pdf = pdf * mask[:, :, None]
+    sig = torch.sigmoid(P._opacity).view(-1, 1, 1)
     d = P._mu - cam.unsqueeze(0)
     dn = d * (1.0 / (torch.sqrt((d * d).sum(dim=1, keepdim=True)) + 1e-8))
-    rho = torch.clamp_min(eval_sh_cuda(deg, sh_features, dn) + 0.5, 0.0).unsqueeze(1)
+    rho = torch.clamp_min(eval_sh_cuda(deg, sh_features, dn) + 0.5, 0.0).view(-1, 1, 1)
     contrib = pdf * sig
-    density = contrib.sum(0).view(nrays, nsamp)
+    density = contrib.sum(0)
     if not use_occlusion:
-        rho_density = (contrib * rho).sum(0).view(nrays, nsamp) * c * deltaT
+        rho_density = (contrib * rho).sum(0) * c * deltaT
         return rho_density, density, torch.ones_like(density)
-    alpha = 1.0 - torch.exp(-contrib * c * deltaT)
-    wa = (alpha * rho).sum(0).view(nrays, nsamp)
-    rd = torch.zeros(nrays, nsamp)
-    de = torch.zeros(nrays, nsamp)
-    tr = torch.zeros(nrays, nsamp)
-    for ri in range(nrays):
-        T = torch.ones(())
-        for s in range(nsamp):
-            de[ri, s] = density[ri, s]
-            tr[ri, s] = T
-            rd[ri, s] = T * wa[ri, s]
-            T = T * torch.exp(-density[ri, s] * c * deltaT)
-            if T.item() < 1e-4:
-                break
-    return rd, de, tr
+    wa = ((1.0 - torch.exp(-contrib * c * deltaT)) * rho).sum(0)
+    step = torch.exp(-density * c * deltaT)
+    T = torch.cumprod(torch.cat([torch.ones(nrays, 1), step[:, :-1]], dim=1), dim=1)
+    live = (T >= 1e-4).float()
+    return T * wa * live, density * live, T * live
+
