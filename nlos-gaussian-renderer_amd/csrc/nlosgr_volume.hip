@@ -490,7 +490,7 @@ __global__ __launch_bounds__(kBlock) void fwd_kernel(KArgs k) {
 // its pair: finished lanes claim owner[slot] with a round stamp, each pair lane gathers its
 // claimant's result with ds_bpermute and folds it into the Gaussian's register accumulators.
 // Losers keep their result and retry next round.  No LDS float atomics, no pair/row tables.
-constexpr int kBSteps = 8;
+constexpr int kBSteps = 16;
 
 struct BwdLayout {
     int wave_base, wave_stride, grow, tth, tph, rayq, owner, pdat, red, total;
@@ -510,12 +510,13 @@ struct BwdLayout {
     }
 };
 
-// per-lane backward segment state (the ray geometry is recomputed from the pair table at finish)
+// per-lane backward segment state
 struct BRay {
     int pos, rem, slot, ij, kl, len;
     float kap, kap0, c0, c2, st;
     float S0, S1, S2;
-    float rho, sigma;                    // netf
+    float zs[3], v[3], ts, w;            // ray geometry for the closed-form result
+    float rho, sigma;
     float T, T0, Etot, pre, dsig, drho;  // netf
     bool ph1;                            // netf: second pass
 };
@@ -543,8 +544,10 @@ __device__ __forceinline__ bool bray_setup(const float* pd, float2 th, float2 ph
     b.c2 = -kHalfLog2e * R.a * dr * dr;
     b.st = th.x;
     b.S0 = b.S1 = b.S2 = 0.f;
+    for (int r = 0; r < 3; ++r) { b.zs[r] = R.zs[r]; b.v[r] = R.v[r]; }
+    b.ts = R.ts;
+    b.w = w; b.rho = rho; b.sigma = sigma;
     if (MODE == NLOSGR_MODE_NETF) {
-        b.rho = rho; b.sigma = sigma;
         b.T = b.T0 = fast_exp2((float)R.kl * f0log2);
         b.Etot = b.pre = b.dsig = b.drho = 0.f;
         b.ph1 = false;
@@ -638,6 +641,7 @@ __global__ __launch_bounds__(kBlock) void bwd_kernel(KArgs k) {
         b.pos = 0; b.rem = 0; b.slot = lane; b.ij = 0; b.kl = 0; b.len = 0;
         b.kap = b.kap0 = b.c0 = b.c2 = b.st = 0.f;
         b.S0 = b.S1 = b.S2 = 0.f;
+        b.zs[0] = b.zs[1] = b.zs[2] = b.v[0] = b.v[1] = b.v[2] = b.ts = b.w = 0.f;
         b.rho = b.sigma = 0.f;
         b.T = b.T0 = b.Etot = b.pre = b.dsig = b.drho = 0.f;
         b.ph1 = false;
@@ -735,25 +739,20 @@ __global__ __launch_bounds__(kBlock) void bwd_kernel(KArgs k) {
                     }
                     if (b.rem <= 0) {
                         // pdf = exp(-|z|^2/2), z = z* + dl v:  dL/du0 = -sum P z,  dL/dv = -sum P dl z
-                        float A[9], u0[3], w, rho, sigma;
-                        load_pdat(pdat + b.slot * 16, A, u0, w, rho, sigma);
-                        const float2 th = tth[b.ij & 0xFFFF], ph = tph[b.ij >> 16];
-                        Ray R;
-                        ray_setup<true>(A, u0, th.x * ph.x, th.x * ph.y, th.y, 0.f, r0, inv_dr, nr, R);
                         float S0 = b.S0, S1 = b.S1 * dr, S2 = b.S2 * dr * dr;
                         if (MODE == NLOSGR_MODE_NOOCL) {
                             if (!RAYS) { S0 *= b.st; S1 *= b.st; S2 *= b.st; }
-                            rSig = S0 * rho;
-                            rRho = S0 * sigma;
-                            S0 *= w; S1 *= w; S2 *= w;
+                            rSig = S0 * b.rho;
+                            rRho = S0 * b.sigma;
+                            S0 *= b.w; S1 *= b.w; S2 *= b.w;
                         } else {
                             rSig = b.dsig;
                             rRho = b.drho;
                         }
                         for (int r = 0; r < 3; ++r) {
-                            const float zv = S0 * R.zs[r] + S1 * R.v[r];
+                            const float zv = S0 * b.zs[r] + S1 * b.v[r];
                             rU[r] = -zv;
-                            rV[r] = -(R.ts * zv + S1 * R.zs[r] + S2 * R.v[r]);
+                            rV[r] = -(b.ts * zv + S1 * b.zs[r] + S2 * b.v[r]);
                         }
                         act = false;
                         pend = true;
