@@ -209,7 +209,7 @@ __device__ __forceinline__ unsigned pack_ray(int slot, int i, int j) {
 // start bins differ — guaranteed per round by a claim table (owner[pos] = lane; losers retry
 // next round).  Lanes that did not win, or ran past their segment, point at private pad bins
 // and add 0, so the step body is branch-free.  Idle lanes are refilled from the ray queue.
-constexpr int kSteps = 8;      // bins per lane per drain round
+constexpr int kSteps = 16;     // bins per lane per drain round
 constexpr int kRefill = 24;    // refill once this many lanes are idle (or the queue is final)
 
 struct FwdLayout {
@@ -529,6 +529,36 @@ __device__ __forceinline__ void load_pdat(const float* pd, float* A, float* u0, 
     w = g.x; rho = g.y; sigma = g.z;
 }
 
+// grow[k] = dL/dhist[p,k] att[k] hscale[p], zero-padded to nr + kBSteps.  Rows of nr % 4 == 0
+// are staged with 16-B loads issued together (one memory round trip per 1024 bins per lane).
+__device__ __forceinline__ void stage_grow(const float* grad, const float* att, float hs, int nr, float* grow) {
+    const int lane = lane_id();
+    if (grad && (nr & 3) == 0 && ((reinterpret_cast<uintptr_t>(grad) | reinterpret_cast<uintptr_t>(att)) & 15) == 0) {
+        const float4* g4 = reinterpret_cast<const float4*>(grad);
+        const float4* a4 = reinterpret_cast<const float4*>(att);
+        const int n4 = nr >> 2;
+        for (int t0 = lane; t0 < n4; t0 += 256) {
+            float4 gv[4], av[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int t = t0 + 64 * u;
+                if (t < n4) { gv[u] = g4[t]; av[u] = a4[t]; }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int t = t0 + 64 * u;
+                if (t < n4)
+                    reinterpret_cast<float4*>(grow)[t] =
+                        make_float4(gv[u].x * av[u].x * hs, gv[u].y * av[u].y * hs, gv[u].z * av[u].z * hs,
+                                    gv[u].w * av[u].w * hs);
+            }
+        }
+    } else {
+        for (int t = lane; t < nr; t += 64) grow[t] = grad ? grad[t] * att[t] * hs : 0.f;
+    }
+    for (int t = nr + lane; t < nr + kBSteps; t += 64) grow[t] = 0.f;
+}
+
 template <int MODE, bool DENSE>
 __device__ __forceinline__ bool bray_setup(const float* pd, float2 th, float2 ph, int slot, int i, int j, int nr,
                                            float mc2, float r0, float dr, float inv_dr, float f0log2, BRay& b) {
@@ -601,10 +631,7 @@ __global__ __launch_bounds__(kBlock) void bwd_kernel(KArgs k) {
         // stage this wall point's upstream gradient row and tables (wave-private)
         const float hs = k.geo.hscale[p];
         wave_sync();
-        for (int t = lane; t < nr + kBSteps; t += 64) {
-            const float g = (k.grad_hist && t < nr) ? k.grad_hist[(size_t)p * nr + t] : 0.f;
-            grow[t] = t < nr ? g * k.geo.att[t] * hs : 0.f;
-        }
+        stage_grow(k.grad_hist ? k.grad_hist + (size_t)p * nr : nullptr, k.geo.att, hs, nr, grow);
         for (int t = lane; t < nt; t += 64)
             tth[t] = make_float2(k.geo.sin_theta[(size_t)p * nt + t], k.geo.cos_theta[(size_t)p * nt + t]);
         for (int t = lane; t < np_; t += 64)
@@ -621,7 +648,7 @@ __global__ __launch_bounds__(kBlock) void bwd_kernel(KArgs k) {
             float mu_[3];
             load_rec(k.recs[gi], P, mu_);
             pair_setup<PRESET, DENSE>(k, gi, mu, px, py, pz, k.geo.grid_lin + 4 * (size_t)p, mc2, P);
-            more = (P.w > 0.f) && P.i0 <= P.i1 && P.j0 <= P.j1;
+            more = (P.w > 0.f) && P.i0 <= P.i1 && P.j0 <= P.j1 && !(k.opt.flags & 2);  // flags 2: setup only
             for (int t = 0; t < 6; ++t) M[t] = P.M[t];
             i0 = P.i0; i1 = P.i1; j0 = P.j0; j1 = P.j1;
             wpair = P.w;
@@ -659,11 +686,11 @@ __global__ __launch_bounds__(kBlock) void bwd_kernel(KArgs k) {
             if (qcount > 0 && (nidle >= kRefill || !anymore)) {
                 const int r = lanes_below(idle);
                 const bool take = !act && !pend && r < qcount;
-                if (take) {
+                if (take && !(k.opt.flags & 1)) {                  // flags 1: enumerate only
                     const unsigned e = rayq[(qhead + r) & (kRQ - 1)];
                     const int slot = e & 0xFF, i = (e >> 8) & 0xFFF, j = e >> 20;
                     act = bray_setup<MODE, DENSE>(pdat + slot * 16, tth[i], tph[j], slot, i, j, nr, mc2, r0, dr,
-                                                  inv_dr, f0log2, b);
+                                                  inv_dr, f0log2, b) && !(k.opt.flags & 4);  // flags 4: no bins
                 }
                 const int ntake = min(nidle, qcount);
                 qhead = (qhead + ntake) & (kRQ - 1);

@@ -1,11 +1,12 @@
-"""Ablation timing of the forward kernel phases (diagnostic; opt.flags bits)."""
+"""Ablation timing of the forward / backward kernel phases (diagnostic opt.flags bits:
+2 = pair setup only, 1 = + candidate enumeration, 4 = + segment records, 0 = everything)."""
 import sys, os, time, json
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, 'nlos-gaussian-renderer_amd')); sys.path.insert(0, ROOT)
 import torch, dataclasses
 from nlosgr import GaussianParams, features_flat
 from nlosgr.volume import Scene, make_config
-from nlosgr.render import render_forward
+from nlosgr.render import render_backward, render_forward
 cfgname = sys.argv[1] if len(sys.argv) > 1 else 'C3'
 sizes = {'C3': (100_000, 128, 1024), 'S1': (20_000, 32, 512)}
 ng, H, T = sizes[cfgname]
@@ -22,4 +23,12 @@ for flags in (0, 4, 1, 2):
     render_forward(*args, cfg); torch.cuda.synchronize()
     t0 = time.perf_counter(); render_forward(*args, cfg); torch.cuda.synchronize()
     res[flags] = (time.perf_counter() - t0) * 1000
-print(json.dumps({'config': cfgname, 'fwd_ms_by_flags': res}))
+hist, _ = render_forward(*args, base)
+grad = torch.randn_like(hist) * 1e-3
+bres = {}
+for flags in (0, 4, 1, 2):
+    cfg = dataclasses.replace(base, flags=flags)
+    render_backward(*args, cfg, grad_hist=grad); torch.cuda.synchronize()
+    t0 = time.perf_counter(); render_backward(*args, cfg, grad_hist=grad); torch.cuda.synchronize()
+    bres[flags] = (time.perf_counter() - t0) * 1000
+print(json.dumps({'config': cfgname, 'fwd_ms_by_flags': res, 'bwd_ms_by_flags': bres}))
