@@ -15,6 +15,7 @@
  *                          gaussian_model/gaussian_model.py:297-364, nlos_helpers.py:192-232
  *   nlosgr_render_bwd   <- CUDARenderFunction.backward gaussian_model/cuda_autograd.py:110-191
  *                          (zeros in the reference; real gradients here) and torch autograd of path T
+ *   nlosgr_rays_analytic <- _C.render_rays_analytic  src/volume_renderer_analytic.cu:178-241
  *   nlosgr_bboxes       <- compute_gaussian_bboxes_kernel include/bbox_compute.cuh:76-120,
  *                          GaussianModel.get_bboxes gaussian_model/gaussian_model.py:140-178
  */
@@ -45,7 +46,10 @@ enum {
 /* per-sample density model */
 enum {
     NLOSGR_MODE_NOOCL = 0, /* rho_d = sum_g sigma pdf rho                  (gaussian_model.py:346-364) */
-    NLOSGR_MODE_NETF = 1   /* per-Gaussian self-transmittance cumprod       (gaussian_model.py:313-324) */
+    NLOSGR_MODE_NETF = 1,  /* per-Gaussian self-transmittance cumprod       (gaussian_model.py:313-324) */
+    NLOSGR_MODE_BININT = 2 /* no-occlusion with each sample replaced by the exact average of the pdf
+                              over its radial bin [r_k -+ dr/2] (closed-form erf; forward only) — the
+                              corrected counterpart of the analytic section path */
 };
 
 enum {
@@ -167,6 +171,19 @@ NLOSGR_API int nlosgr_rays_bwd(const nlosgr_gaussians* g, const nlosgr_rays* r, 
                     float c_deltaT, int32_t use_occlusion, void* workspace, const float* g_rho,
                     const float* g_density, const float* g_trans, float* d_mu, float* d_scaling,
                     float* d_rotation, float* d_opacity, float* d_features, void* hip_stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Path A "analytic section" API (_C.render_rays_analytic, bindings.cpp:6-24,
+ * src/volume_renderer_analytic.cu:178-241): hist_out [nrays] = one value per ray.
+ * Per ray: the first 128 filter entries whose sigma_threshold-ellipsoid the line o + t d hits,
+ * clipped to [t_min, t_max], stably sorted by entry, composited front to back with the
+ * reference's closed-form optical depth (analytic_integration.cuh:123-172, formula as written)
+ * and early exit at T < 1e-4.  r->t / r->nsamp are unused; features rows have stride k_feat and
+ * SH is evaluated to g->sh_degree (unsigned basis, spherical_harmonics.cuh:20-80).  Forward only.
+ * ------------------------------------------------------------------------------------- */
+NLOSGR_API int nlosgr_rays_analytic(const nlosgr_gaussians* g, const nlosgr_rays* r, const int32_t* filter,
+                         float t_min, float t_max, float sigma_threshold, float* hist_out,
+                         void* hip_stream);
 
 NLOSGR_API const char* nlosgr_last_error(void);
 NLOSGR_API int nlosgr_abi_version(void);

@@ -1,0 +1,195 @@
+// Path A "analytic section" renderer (gfx950): one value per ray, the semantics of the
+// reference's _C.render_rays_analytic (src/volume_renderer_analytic.cu:23-241 with
+// include/analytic_integration.cuh:38-192), which SectionGaussianRendererCUDA.render_transient
+// (submodules/cuda_renderer/section_renderer.py:55-186) places in the middle bin.
+//
+//   wave = one ray (4 rays per 256-thread workgroup).
+//   1. sections: lanes take the ray's filter row 64 entries at a time; each lane intersects the
+//      line with its Gaussian's sigma-ellipsoid (compute_gaussian_section :38-104), clips the
+//      interval to [t_min, t_max] and ballot-compacts the hits; the first 128 hits in filter
+//      order are kept (the reference's loop bound, volume_renderer_analytic.cu:73).
+//   2. stable sort by t_enter (insertion sort :178-192) as a rank computation: rank = #smaller
+//      + #equal-and-earlier, two sections per lane, keys broadcast from LDS.
+//   3. per sorted section (lane-parallel): the reference's closed-form tau (:123-172, formula as
+//      written) and the SH albedo; then one lane composites front to back in the reference's
+//      order and precision (acc += T (1 - e^-tau) rho, T *= e^-tau, stop once T < 1e-4).
+// All arithmetic is IEEE fp32 with the reference's expression order (no fast-math intrinsics):
+// this is the parity path, not a throughput path (per ray it touches at most 256 Gaussians).
+#include "nlosgr_common.hpp"
+
+using namespace nlosgr;
+using namespace nlosgr::detail;
+
+namespace {
+
+constexpr int kMaxPerRay = NLOSGR_MAX_PER_RAY;   // filter row: count + 256 indices
+constexpr int kRowLen = kMaxPerRay + 1;
+constexpr int kMaxSec = 128;                     // MAX_SECTIONS_PER_RAY (volume_renderer_analytic.cu:11)
+constexpr int kAWaves = 4;
+
+struct SecWave {
+    float te[kMaxSec], tx[kMaxSec];   // sections in filter order
+    int gi[kMaxSec];
+    int sg[kMaxSec];                  // sorted
+    float ste[kMaxSec], stx[kMaxSec];
+    float tau[kMaxSec], rho[kMaxSec];
+};
+
+struct Local {
+    float so[3], sd[3], s[3];
+};
+
+// Ray in the Gaussian's frame, scaled by 1/s (s = exp(S) mod, no eps; R from quat_to_rotmat,
+// cuda_utils.cuh:54-85; local = R^T (x - mu), analytic_integration.cuh:53-83).
+__device__ __forceinline__ void to_local(const nlosgr_gaussians& g, int gi, const float* o, const float* d,
+                                         Local& L) {
+    for (int t = 0; t < 3; ++t) L.s[t] = expf(g.scaling[3 * gi + t]) * g.scaling_modifier;
+    float w = g.rotation[4 * gi], x = g.rotation[4 * gi + 1], y = g.rotation[4 * gi + 2], z = g.rotation[4 * gi + 3];
+    float R[9];
+    const float nrm = sqrtf(w * w + x * x + y * y + z * z);
+    if (nrm < 1e-8f) {
+        R[0] = 1.f; R[1] = 0.f; R[2] = 0.f; R[3] = 0.f; R[4] = 1.f; R[5] = 0.f; R[6] = 0.f; R[7] = 0.f; R[8] = 1.f;
+    } else {
+        w /= nrm; x /= nrm; y /= nrm; z /= nrm;
+        quat_rot(w, x, y, z, R);
+    }
+    const float q[3] = {o[0] - g.mu[3 * gi], o[1] - g.mu[3 * gi + 1], o[2] - g.mu[3 * gi + 2]};
+    for (int c = 0; c < 3; ++c) {
+        const float lo = R[c] * q[0] + R[3 + c] * q[1] + R[6 + c] * q[2];
+        const float ld = R[c] * d[0] + R[3 + c] * d[1] + R[6 + c] * d[2];
+        L.sd[c] = ld / L.s[c];
+        L.so[c] = lo / L.s[c];
+    }
+}
+
+__device__ __forceinline__ float dot3(const float* a, const float* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+
+__global__ __launch_bounds__(kBlock) void analytic_kernel(nlosgr_gaussians g, nlosgr_rays r, const int32_t* filter,
+                                                        float t_min, float t_max, float sig_thr,
+                                                        float* __restrict__ out) {
+    __shared__ SecWave sm[kAWaves];
+    const int wave = threadIdx.x >> 6, lane = lane_id();
+    const int ray = blockIdx.x * kAWaves + wave;
+    if (ray >= r.nrays) return;                     // wave-uniform: no workgroup barrier below
+    SecWave& S = sm[wave];
+    const float o[3] = {r.origins[3 * ray], r.origins[3 * ray + 1], r.origins[3 * ray + 2]};
+    const float d[3] = {r.dirs[3 * ray], r.dirs[3 * ray + 1], r.dirs[3 * ray + 2]};
+    const int32_t* row = filter + (size_t)ray * kRowLen;
+    const int n = min(max(row[0], 0), kMaxPerRay);
+
+    // 1. sections in filter order (first kMaxSec hits)
+    int nsec = 0;
+    for (int e0 = 0; e0 < n && nsec < kMaxSec; e0 += 64) {
+        const int e = e0 + lane;
+        bool hit = false;
+        float te = 0.f, tx = 0.f;
+        int gi = -1;
+        if (e < n) {
+            gi = row[1 + e];
+            if (gi >= 0 && gi < g.ng) {
+                Local L;
+                to_local(g, gi, o, d, L);
+                const float a = dot3(L.sd, L.sd);
+                const float b = 2.0f * dot3(L.so, L.sd);
+                const float c = dot3(L.so, L.so) - sig_thr * sig_thr;
+                const float disc = b * b - 4.0f * a * c;
+                if (disc >= 0.0f) {
+                    const float sq = sqrtf(disc);
+                    te = fmaxf((-b - sq) / (2.0f * a), t_min);
+                    tx = fminf((-b + sq) / (2.0f * a), t_max);
+                    hit = te < tx;
+                }
+            }
+        }
+        const unsigned long long m = __builtin_amdgcn_ballot_w64(hit);
+        const int pos = nsec + lanes_below(m);
+        if (hit && pos < kMaxSec) {
+            S.te[pos] = te;
+            S.tx[pos] = tx;
+            S.gi[pos] = gi;
+        }
+        nsec = min(nsec + (int)__popcll(m), kMaxSec);
+    }
+    wave_sync();
+
+    // 2. stable sort by t_enter: rank = #{t_j < t_i} + #{j < i : t_j == t_i}
+    for (int i = lane; i < nsec; i += 64) {
+        const float ti = S.te[i];
+        int rank = 0;
+        for (int j = 0; j < nsec; ++j) {
+            const float tj = S.te[j];
+            rank += (tj < ti || (tj == ti && j < i)) ? 1 : 0;
+        }
+        S.sg[rank] = S.gi[i];
+        S.ste[rank] = ti;
+        S.stx[rank] = S.tx[i];
+    }
+    wave_sync();
+
+    // 3. tau and albedo per sorted section (compute_analytic_transmittance :123-172; :146-151)
+    for (int s = lane; s < nsec; s += 64) {
+        const int gi = S.sg[s];
+        Local L;
+        to_local(g, gi, o, d, L);
+        const float a = dot3(L.so, L.so);
+        const float b = 2.0f * dot3(L.so, L.sd);
+        const float c = dot3(L.sd, L.sd);
+        const float opac = 1.0f / (1.0f + expf(-g.opacity[gi]));
+        // sqrtf(2.0f * M_PI / c): the quotient is formed in double in the reference
+        const float G = opac * sqrtf((float)(2.0 * 3.14159265358979323846 / (double)c)) * L.s[0] * L.s[1] * L.s[2];
+        const float ef = expf(-0.5f * (a - b * b / (4.0f * c)));
+        const float rc = 2.0f * sqrtf(c);
+        const float e1 = erff((b + 2.0f * c * S.stx[s]) / rc);
+        const float e0 = erff((b + 2.0f * c * S.ste[s]) / rc);
+        S.tau[s] = fmaxf(G * ef * (e1 - e0), 0.0f);
+        float vx, vy, vz, nrm;
+        view_dir<NLOSGR_PRESET_CUDA>(g.mu[3 * gi] - r.cam[0], g.mu[3 * gi + 1] - r.cam[1], g.mu[3 * gi + 2] - r.cam[2],
+                                     vx, vy, vz, nrm);
+        float Y[kMaxK];
+        sh_basis<NLOSGR_PRESET_CUDA>(g.sh_degree, vx, vy, vz, Y);
+        const int K = (g.sh_degree + 1) * (g.sh_degree + 1);
+        const float* f = g.features + (size_t)gi * g.k_feat;
+        float sh = 0.f;
+        for (int k = 0; k < K; ++k) sh += f[k] * Y[k];
+        S.rho[s] = fmaxf(sh + 0.5f, 0.0f);
+    }
+    wave_sync();
+
+    // 4. front-to-back compositing in the reference's order (:118-170)
+    if (lane == 0) {
+        float T = 1.0f, acc = 0.0f;
+        for (int s = 0; s < nsec; ++s) {
+            const float st = expf(-S.tau[s]);
+            acc += T * (1.0f - st) * S.rho[s];
+            T *= st;
+            if (T < 1e-4f) break;
+        }
+        out[ray] = acc;
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int nlosgr_rays_analytic(const nlosgr_gaussians* g, const nlosgr_rays* r, const int32_t* filter, float t_min,
+                         float t_max, float sigma_threshold, float* hist_out, void* hip_stream) {
+    if (!g || !r) return set_err(NLOSGR_E_INVALID, "null argument struct");
+    if (g->ng < 0 || r->nrays < 0) return set_err(NLOSGR_E_INVALID, "negative size");
+    if (g->sh_degree < 0 || g->sh_degree > 3)
+        return set_err(NLOSGR_E_UNSUPPORTED, "active_sh_degree must be in [0, 3]");
+    if (g->k_feat < (g->sh_degree + 1) * (g->sh_degree + 1) || g->k_feat > kMaxK)
+        return set_err(NLOSGR_E_INVALID, "k_feat must satisfy (sh_degree+1)^2 <= k_feat <= 16");
+    if (r->nrays == 0) return NLOSGR_OK;
+    if (!r->origins || !r->dirs || !r->cam || !filter || !hist_out)
+        return set_err(NLOSGR_E_INVALID, "null ray/filter/output pointer");
+    if (g->ng > 0 && (!g->mu || !g->scaling || !g->rotation || !g->opacity || !g->features))
+        return set_err(NLOSGR_E_INVALID, "null Gaussian parameter pointer");
+    hipStream_t s = (hipStream_t)hip_stream;
+    hipLaunchKernelGGL(analytic_kernel, dim3((r->nrays + kAWaves - 1) / kAWaves), dim3(kBlock), 0, s, *g, *r, filter,
+                       t_min, t_max, sigma_threshold, hist_out);
+    HIPCHK(hipGetLastError());
+    return NLOSGR_OK;
+}
+
+}  // extern "C"

@@ -232,6 +232,7 @@ struct Drain {
     float ga, al;     // log2 value(t) = ga t^2 + al   (noocl: al includes log2 w [+ log2 sin theta])
     float st;         // sin(theta_i) (kept separate only when per-ray outputs are written)
     float sc, lwc, logT;  // netf: sigma c dT, log2(w c dT), log2 T at pos
+    float beta, xlo, elo; // binint: dr sqrt(a/2), lower bin edge beta (kap - 1/2) and erfc(|xlo|)
     int rbase;        // RAYS: ray * nr
 };
 
@@ -249,6 +250,14 @@ __device__ __forceinline__ bool drain_setup(const float* A, const float* u0, flo
         d.al = fmaf(-kHalfLog2e, R.m2min, lw);
         if (!RAYS) d.al += flog2(th.x);
         d.st = th.x;
+    } else if (MODE == NLOSGR_MODE_BININT) {
+        // bin average of exp(-a (r - t*)^2 / 2) over [r_k -+ dr/2] = sqrt(pi)/(2 beta) (erf(x1) - erf(x0))
+        d.beta = dr * sqrtf(0.5f * R.a);
+        d.al = fmaf(-kHalfLog2e, R.m2min, lw) + log2f(0.88622692545275801f / d.beta);
+        if (!RAYS) d.al += flog2(th.x);
+        d.st = th.x;
+        d.xlo = d.beta * (d.t - 0.5f);
+        d.elo = erfcf(fabsf(d.xlo));
     } else {
         d.al = -kHalfLog2e * R.m2min;
         d.sc = sc;
@@ -351,6 +360,7 @@ __global__ __launch_bounds__(kBlock) void fwd_kernel(KArgs k) {
     Drain d;
     d.pos = 0; d.rem = 0; d.t = 0.f; d.ga = 0.f; d.al = 0.f; d.st = 0.f;
     d.sc = 0.f; d.lwc = 0.f; d.logT = 0.f; d.rbase = 0;
+    d.beta = 0.f; d.xlo = 0.f; d.elo = 0.f;
     bool act = false;
     int qhead = 0, qcount = 0;
 
@@ -426,6 +436,7 @@ __global__ __launch_bounds__(kBlock) void fwd_kernel(KArgs k) {
             float* hb = hist + (win ? d.pos : pad);
             float t = d.t;
             float logT = d.logT;
+            float xlo = d.xlo, elo = d.elo;
 #pragma unroll
             for (int m = 0; m < kSteps; ++m) {
                 const bool in = m < remw;
@@ -433,6 +444,19 @@ __global__ __launch_bounds__(kBlock) void fwd_kernel(KArgs k) {
                 float v;
                 if (MODE == NLOSGR_MODE_NOOCL) {
                     const float pv = fast_exp2(e2);
+                    v = in ? pv : 0.f;
+                    if (RAYS) {
+                        if (in) atomicAdd(rout + d.rbase + d.pos + m, rscale * pv);
+                        v *= d.st;
+                    }
+                } else if (MODE == NLOSGR_MODE_BININT) {
+                    // erf(x1) - erf(x0) from erfc of |x| (no cancellation in the tails)
+                    const float x1 = d.beta * (t + 0.5f);
+                    const float e1 = erfcf(fabsf(x1));
+                    const float df = xlo >= 0.f ? elo - e1 : (x1 <= 0.f ? e1 - elo : 2.0f - elo - e1);
+                    xlo = x1;
+                    elo = e1;
+                    const float pv = fast_exp2(d.al) * df;
                     v = in ? pv : 0.f;
                     if (RAYS) {
                         if (in) atomicAdd(rout + d.rbase + d.pos + m, rscale * pv);
@@ -454,6 +478,8 @@ __global__ __launch_bounds__(kBlock) void fwd_kernel(KArgs k) {
             if (win) {
                 d.t = t;
                 d.logT = logT;
+                d.xlo = xlo;
+                d.elo = elo;
                 d.pos += kSteps;
                 d.rem -= kSteps;
                 act = d.rem > 0;
@@ -934,7 +960,7 @@ int validate(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr
         return set_err(NLOSGR_E_UNSUPPORTED, "active_sh_degree must be in [0, 3]");
     if (g->k_feat < (g->sh_degree + 1) * (g->sh_degree + 1) || g->k_feat > kMaxK)
         return set_err(NLOSGR_E_INVALID, "k_feat must satisfy (sh_degree+1)^2 <= k_feat <= 16");
-    if (opt->mode != NLOSGR_MODE_NOOCL && opt->mode != NLOSGR_MODE_NETF)
+    if (opt->mode != NLOSGR_MODE_NOOCL && opt->mode != NLOSGR_MODE_NETF && opt->mode != NLOSGR_MODE_BININT)
         return set_err(NLOSGR_E_INVALID, "unknown mode");
     if (geo->nwall < 0 || geo->nt < 1 || geo->np < 1 || geo->nr < 1)
         return set_err(NLOSGR_E_INVALID, "bad geometry sizes");
@@ -1012,10 +1038,12 @@ int run_fwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_
     const bool rays = ray_out != nullptr;
     if (g->preset == NLOSGR_PRESET_TORCH) {
         if (opt->mode == NLOSGR_MODE_NOOCL) dispatch_fwd<0, 0>(ka, dense, rays, shm, s);
-        else dispatch_fwd<0, 1>(ka, dense, rays, shm, s);
+        else if (opt->mode == NLOSGR_MODE_NETF) dispatch_fwd<0, 1>(ka, dense, rays, shm, s);
+        else dispatch_fwd<0, 2>(ka, dense, rays, shm, s);
     } else {
         if (opt->mode == NLOSGR_MODE_NOOCL) dispatch_fwd<1, 0>(ka, dense, rays, shm, s);
-        else dispatch_fwd<1, 1>(ka, dense, rays, shm, s);
+        else if (opt->mode == NLOSGR_MODE_NETF) dispatch_fwd<1, 1>(ka, dense, rays, shm, s);
+        else dispatch_fwd<1, 2>(ka, dense, rays, shm, s);
     }
     HIPCHK(hipGetLastError());
     return NLOSGR_OK;
@@ -1061,6 +1089,8 @@ int nlosgr_render_bwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo, con
                       void* hip_stream) {
     int rc = validate(g, geo, opt);
     if (rc) return rc;
+    if (opt->mode == NLOSGR_MODE_BININT)
+        return set_err(NLOSGR_E_UNSUPPORTED, "no backward for the bin-integrated (analytic) forward");
     if (g->ng == 0) return NLOSGR_OK;
     if (!workspace) return set_err(NLOSGR_E_INVALID, "workspace is null");
     if (!d_mu || !d_scaling || !d_rotation || !d_opacity || !d_features)

@@ -16,8 +16,9 @@ PRESET_TORCH = 0
 PRESET_CUDA = 1
 MODE_NOOCL = 0
 MODE_NETF = 1
+MODE_BININT = 2
 PRESETS = {"torch": PRESET_TORCH, "cuda": PRESET_CUDA}
-MODES = {"noocl": MODE_NOOCL, "netf": MODE_NETF}
+MODES = {"noocl": MODE_NOOCL, "netf": MODE_NETF, "binint": MODE_BININT}
 
 _P = ctypes.c_void_p
 
@@ -50,7 +51,7 @@ MAX_PER_RAY = 256   # NLOSGR_MAX_PER_RAY
 # every symbol include/nlosgr.h declares (tests check the exports against this list)
 EXPORTS = ["nlosgr_workspace_bytes", "nlosgr_render_fwd", "nlosgr_render_bwd", "nlosgr_count_support",
            "nlosgr_bboxes", "nlosgr_rays_workspace_bytes", "nlosgr_filter_rays", "nlosgr_rays_fwd",
-           "nlosgr_rays_bwd", "nlosgr_last_error", "nlosgr_abi_version"]
+           "nlosgr_rays_bwd", "nlosgr_rays_analytic", "nlosgr_last_error", "nlosgr_abi_version"]
 
 _lib = None
 _load_error = None
@@ -84,6 +85,8 @@ def load():
     lib.nlosgr_rays_bwd.argtypes = [PG, PR, _P, ctypes.c_float, ctypes.c_int32, _P, _P, _P, _P, _P, _P, _P,
                                     _P, _P, _P]
     lib.nlosgr_rays_bwd.restype = ctypes.c_int
+    lib.nlosgr_rays_analytic.argtypes = [PG, PR, _P, ctypes.c_float, ctypes.c_float, ctypes.c_float, _P, _P]
+    lib.nlosgr_rays_analytic.restype = ctypes.c_int
     lib.nlosgr_bboxes.argtypes = [PG, ctypes.c_float, _P, _P]
     lib.nlosgr_bboxes.restype = ctypes.c_int
     lib.nlosgr_last_error.argtypes = []

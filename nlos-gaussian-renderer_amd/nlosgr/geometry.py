@@ -123,7 +123,7 @@ def build_geometry(walls, box, ns, start, end, c, deltaT, volume_y, preset="torc
     box = box.to(device).float()
     tmin, tmax, pmin, pmax = angle_ranges(walls, box)
     extra = float(volume_y) ** 2                 # x Y^2, nlos_helpers.py:226 / :275-276
-    if preset == "cuda" and mode == "noocl":
+    if preset == "cuda" and mode in ("noocl", "binint"):
         extra = extra * (c * deltaT)             # volume_renderer.cu:182 (x c dT in-kernel)
     r, att, _, _ = radial_tables(start, end, c, deltaT, preset, device)
     return geometry_from_ranges(walls, tmin, tmax, pmin, pmax, ns, ns, r, att, extra)

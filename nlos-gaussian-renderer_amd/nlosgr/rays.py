@@ -106,3 +106,30 @@ def render_rays(ray_origins, ray_directions, t_samples, gaussian_means, gaussian
     return rays_forward(ray_origins, ray_directions, t_samples, gaussian_means, gaussian_scales,
                         gaussian_rotations, gaussian_opacities, gaussian_features, camera_pos, active_sh_degree,
                         c * deltaT, scaling_modifier, use_occlusion, filt, preset)
+
+
+def render_rays_analytic(ray_origins, ray_directions, t_min, t_max, gaussian_filter, gaussian_means,
+                         gaussian_scales, gaussian_rotations, gaussian_opacities, gaussian_features, camera_pos,
+                         active_sh_degree, c, deltaT, scaling_modifier, sigma_threshold, rendering_type="netf"):
+    """_C.render_rays_analytic (bindings.cpp:6-24, volume_renderer_analytic.cu:178-241): [N_rays]
+    one value per ray from the sections of the filtered Gaussians.  c, deltaT and rendering_type
+    are accepted and unused, as in the reference kernel.  Forward only (the reference has no
+    backward for this path)."""
+    if rendering_type not in ("netf", "nlos-neus"):
+        raise ValueError(f"unknown rendering_type {rendering_type!r}")
+    lib = _lib.load()
+    ro, rd, cam = [_as_f32(x) for x in (ray_origins, ray_directions, camera_pos)]
+    means, scales, rotations, opacities, features = [_as_f32(x) for x in (gaussian_means, gaussian_scales,
+                                                                           gaussian_rotations, gaussian_opacities,
+                                                                           gaussian_features)]
+    filt = gaussian_filter.detach()
+    if filt.dtype != torch.int32 or filt.dim() != 2 or filt.shape != (ro.shape[0], _lib.MAX_PER_RAY + 1):
+        raise ValueError("gaussian_filter must be int32 [N_rays, 257] (filter_gaussians_per_ray layout)")
+    filt = filt.contiguous()
+    t = torch.zeros(1, device=ro.device)
+    g, r, _ = _structs(ro, rd, t, cam, means, scales, rotations, opacities, features, active_sh_degree,
+                       scaling_modifier, "cuda")
+    out = torch.empty(ro.shape[0], device=ro.device)
+    _lib.check(lib.nlosgr_rays_analytic(g, r, _lib.ptr(filt), float(t_min), float(t_max), float(sigma_threshold),
+                                        _lib.ptr(out), _lib.stream_handle(ro.device)))
+    return out

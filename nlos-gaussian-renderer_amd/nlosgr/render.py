@@ -18,7 +18,7 @@ from . import _lib
 @dataclass(frozen=True)
 class RenderConfig:
     preset: str = "torch"        # "torch" (path T) or "cuda" (path C)
-    mode: str = "noocl"          # "noocl" or "netf"
+    mode: str = "noocl"          # "noocl", "netf" or "binint" (bin-integrated no-occlusion, forward only)
     sh_degree: int = 0
     scaling_modifier: float = 1.0
     cutoff: float = 0.0          # Mahalanobis support radius; <= 0 -> dense

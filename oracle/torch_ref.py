@@ -362,3 +362,144 @@ def render_rays_cuda(ray_o, ray_d, t, P, sh_features, cam, deg, c, deltaT, mod, 
     live = (T >= 1e-4).float()
     return T * wa * live, density * live, T * live
 
+
+
+# --------------------------------------------------------------------------------------------
+# C4 "analytic_exact": per-bin exact integral of the numerical model (not a reference function;
+# SURVEY §8d C4 — the corrected counterpart of the analytic section path, cross-checked against
+# the point-sampled numerical path at the same support)
+# --------------------------------------------------------------------------------------------
+def _erf_diff(x0, x1):
+    """erf(x1) - erf(x0) for x0 <= x1 without tail cancellation (erfc on the far side)."""
+    e0, e1 = torch.special.erfc(x0.abs()), torch.special.erfc(x1.abs())
+    return torch.where(x0 >= 0, e0 - e1, torch.where(x1 <= 0, e1 - e0, 2.0 - e0 - e1))
+
+
+def bin_integrated_pdf(P, p, tab, preset="cuda", mod=1.0, mc=None):
+    """[Ng, Na] in the (k, i, j) order of input_points: the average of pdf_g over the radial bin
+    [r_k - dr/2, r_k + dr/2] of ray (i, j), in float64.  Along a ray u(r) = u0 + r v, so
+    pdf = exp(-m2min/2) exp(-a (r - t*)^2 / 2) and the bin average is
+    exp(-m2min/2) sqrt(pi)/(2 beta) [erf(beta (kap + 1/2)) - erf(beta (kap - 1/2))],
+    beta = dr sqrt(a/2), kap = (r_k - t*)/dr.  The support mask is the numerical path's
+    (m^2 at the bin centre <= mc^2, gaussian_pdf)."""
+    f64 = torch.float64
+    theta, phi, r = tab["theta"].to(f64), tab["phi"].to(f64), tab["r"].to(f64)
+    ns, nr = theta.shape[0], r.shape[0]
+    dirs = torch.stack([torch.sin(theta)[:, None] * torch.cos(phi)[None, :],
+                        torch.sin(theta)[:, None] * torch.sin(phi)[None, :],
+                        torch.cos(theta)[:, None].expand(ns, ns)], dim=-1).reshape(-1, 3)   # [ns*ns, 3]
+    if preset == "torch":
+        s = torch.exp(torch.exp(P._scaling) * mod).to(f64)
+        Rot = build_rotation(torch.nn.functional.normalize(P._rotation)).to(f64)
+    else:
+        s = (torch.exp(P._scaling) * mod + 1e-8).to(f64)
+        Rot = quat_to_rotmat_cuda(P._rotation).transpose(1, 2).to(f64)
+    mu = P._mu.to(f64)
+    u0 = torch.einsum("gab,gb->ga", Rot, p.to(f64)[None, :] - mu) / s                 # [Ng, 3]
+    v = torch.einsum("gab,nb->gna", Rot, dirs) / s[:, None, :]                         # [Ng, R, 3]
+    a = (v * v).sum(-1)
+    ts = -(u0[:, None, :] * v).sum(-1) / a
+    zs = u0[:, None, :] + ts[..., None] * v
+    m2min = (zs * zs).sum(-1)
+    dr = (r[-1] - r[0]) / (nr - 1)
+    beta = dr * torch.sqrt(a / 2)                                                      # [Ng, R]
+    kap = (r[None, :, None] - ts[:, None, :]) / dr                                     # [Ng, nr, R]
+    diff = _erf_diff(beta[:, None, :] * (kap - 0.5), beta[:, None, :] * (kap + 0.5))
+    val = torch.exp(-0.5 * m2min)[:, None, :] * math.sqrt(math.pi) / (2 * beta[:, None, :]) * diff
+    val = val.reshape(P._mu.shape[0], -1)
+    if mc is not None:
+        live = gaussian_pdf(tab["input_points"][:, 0:3], P, preset, mod, mc) > 0
+        val = torch.where(live, val, torch.zeros_like(val))
+    return val
+
+
+def render_volume_binint(P, walls, box, Y, ns, start, end, c, deltaT, preset="cuda", mod=1.0, mc=None):
+    """hist [P, Nr] of the no-occlusion path with bin_integrated_pdf in place of the point pdf
+    (attenuation, sin(theta), angular sum and scales exactly as render_wallpoint)."""
+    hs = []
+    for w in range(walls.shape[0]):
+        p = walls[w]
+        tab = sample_tables(p, box, ns, start, end, c, deltaT)
+        nr = tab["r"].shape[0]
+        pdf = bin_integrated_pdf(P, p, tab, preset, mod, mc)
+        sig = torch.sigmoid(P._opacity).to(torch.float64)
+        rho = albedo(P, p, preset).to(torch.float64)
+        rd = torch.sum(pdf * sig * rho, dim=0)
+        if preset == "cuda":
+            rd = rd * c * deltaT
+        result = rd.reshape(nr, ns * ns)
+        theta_grid = tab["input_points"].view(-1, ns * ns, 5)[:, :, 3].to(torch.float64)
+        if preset == "torch":
+            dist = (torch.linspace(tab["I1"], tab["I2"], nr, dtype=torch.float) * deltaT * c).view(-1, 1)
+            result = result / (dist.to(torch.float64) ** 2) * torch.sin(theta_grid)
+        else:
+            t = torch.linspace(tab["I1"] * c * deltaT, tab["I2"] * c * deltaT, nr).view(-1, 1)
+            result = result / (t.to(torch.float64) ** 2 + 1e-8) * torch.sin(theta_grid)
+        hs.append(torch.sum(result * Y ** 2, dim=1) * tab["dtheta"] * tab["dphi"])
+    return torch.stack(hs)
+
+
+# --------------------------------------------------------------------------------------------
+# path A: the analytic section renderer (_C.render_rays_analytic)
+# --------------------------------------------------------------------------------------------
+def render_rays_analytic(ray_o, ray_d, t_min, t_max, filt, P, sh_features, cam, deg, mod=1.0, sigma=3.0):
+    """One value per ray, volume_renderer_analytic.cu:23-173 with analytic_integration.cuh:38-192.
+
+    Per ray: the first 128 filter entries (in filter order) whose sigma-ellipsoid the line hits
+    (compute_gaussian_section :38-104; s = exp(S) mod with no eps, local = R^T (x - mu)), entry/exit
+    clipped to [t_min, t_max] and kept iff t_enter < t_exit; stable sort by t_enter (insertion sort
+    :178-192); per section tau = max(0, G e^{-(a - b^2/4c)/2} [erf((b + 2c t1)/(2 sqrt c)) -
+    erf((b + 2c t0)/(2 sqrt c))]), G = sigma_o sqrt(2 pi / c) sx sy sz (:123-172, the reference's
+    formula as written); acc += T (1 - e^-tau) rho, T *= e^-tau, stop once T < 1e-4 (:118-170).
+    rho = max(0, 0.5 + SH_cuda(deg, f_g, normalize_eps(mu - cam))) (:148-151).  Pure-Python loop
+    over rays: small cases only."""
+    ng = P._mu.shape[0]
+    out = torch.zeros(ray_o.shape[0])
+    s_all = torch.exp(P._scaling) * mod
+    R_all = quat_to_rotmat_cuda(P._rotation)
+    sig_all = torch.sigmoid(P._opacity).reshape(-1)
+    d = P._mu - cam[None, :]
+    dn = d * (1.0 / (torch.sqrt((d * d).sum(dim=1, keepdim=True)) + 1e-8))
+    rho_all = torch.clamp_min(eval_sh_cuda(deg, sh_features, dn) + 0.5, 0.0)
+    for ray in range(ray_o.shape[0]):
+        o, dv = ray_o[ray], ray_d[ray]
+        n = int(filt[ray, 0])
+        secs = []
+        for e in range(n):
+            if len(secs) >= 128:
+                break
+            g = int(filt[ray, 1 + e])
+            if g < 0 or g >= ng:
+                continue
+            Rt = R_all[g].t()
+            so = (Rt @ (o - P._mu[g])) / s_all[g]
+            sd = (Rt @ dv) / s_all[g]
+            a = torch.dot(sd, sd)
+            b = 2.0 * torch.dot(so, sd)
+            cc = torch.dot(so, so) - sigma * sigma
+            disc = b * b - 4.0 * a * cc
+            if disc < 0:
+                continue
+            sq = torch.sqrt(disc)
+            te = torch.clamp_min((-b - sq) / (2.0 * a), t_min)
+            tx = torch.clamp_max((-b + sq) / (2.0 * a), t_max)
+            if te < tx:
+                secs.append((g, float(te), float(tx), so, sd))
+        secs.sort(key=lambda x: x[1])   # stable, as the insertion sort
+        T, acc = 1.0, 0.0
+        for g, te, tx, so, sd in secs:
+            A = torch.dot(so, so)
+            B = 2.0 * torch.dot(so, sd)
+            C = torch.dot(sd, sd)
+            G = sig_all[g] * torch.sqrt(2.0 * math.pi / C) * s_all[g].prod()
+            ef = torch.exp(-0.5 * (A - B * B / (4.0 * C)))
+            e1 = torch.special.erf((B + 2.0 * C * tx) / (2.0 * torch.sqrt(C)))
+            e0 = torch.special.erf((B + 2.0 * C * te) / (2.0 * torch.sqrt(C)))
+            tau = torch.clamp_min(G * ef * (e1 - e0), 0.0)
+            st = torch.exp(-tau)
+            acc = acc + T * (1.0 - st) * rho_all[g]
+            T = T * st
+            if T < 1e-4:
+                break
+        out[ray] = acc
+    return out

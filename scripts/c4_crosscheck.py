@@ -1,0 +1,72 @@
+"""C4 (BASELINE.json configs[3]): analytic (per-bin exact erf integral, mode "binint") vs the
+numerical point-sampled path on the C3 inputs (100k Gaussians -> 128x128x1024, cuda preset),
+forward only, on one MI355X.  Prints one JSON line: relative L2 and max error per volume for each
+support cutoff, the stated tolerance, and the forward time of both paths.
+
+    python scripts/c4_crosscheck.py [--cutoffs 3,5] [--ng 100000] [--hw 128] [--t 1024]
+
+Tolerance: the bin average differs from the point sample by ~ (dr^2 a / 24)(1 - a dr^2 kap^2)
+per ray segment, a = 1/sigma_r^2 along the ray, so per volume the relative L2 is
+~ (dr / sigma)^2 / 24; stated bound = (dr / s_min)^2 / 24 with s_min the smallest Gaussian scale
+(<= 1e-2 for sigma/dr >= 4).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "nlos-gaussian-renderer_amd"))
+
+import torch  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--cutoffs", default="3,5")
+    ap.add_argument("--ng", type=int, default=100_000)
+    ap.add_argument("--hw", type=int, default=128)
+    ap.add_argument("--t", type=int, default=1024)
+    a = ap.parse_args()
+    from nlosgr import GaussianParams
+    from nlosgr.model import features_flat
+    from nlosgr.render import render_forward
+    from nlosgr.volume import Scene, make_config
+    dev = torch.device("cuda:0")
+    scene = Scene(H=a.hw, W=a.hw, T=a.t, ns=32)
+    m = GaussianParams.synthetic(a.ng, 3, preset="cuda", device=dev, seed=0)
+    params = [m._mu.detach(), m._scaling.detach(), m._rotation.detach(), m._opacity.detach(),
+              features_flat(m).detach().contiguous()]
+    geo_n = scene.geometry(dev, "cuda", "noocl")
+    geo_b = scene.geometry(dev, "cuda", "binint")
+    dr = (geo_n.r[-1] - geo_n.r[0]).item() / (a.t - 1)
+    s = torch.exp(m._scaling.detach())
+    s_min, s_med = s.min().item(), s.median().item()
+
+    def timed(geo, cfg):
+        render_forward(*params, geo, cfg)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        h, _ = render_forward(*params, geo, cfg)
+        torch.cuda.synchronize()
+        return h, (time.perf_counter() - t0) * 1e3
+
+    res = []
+    for mc in [float(x) for x in a.cutoffs.split(",")]:
+        h_n, t_n = timed(geo_n, make_config(m, scene, mode="noocl", cutoff=mc))
+        h_b, t_b = timed(geo_b, make_config(m, scene, mode="binint", cutoff=mc))
+        d = h_b - h_n
+        res.append({"cutoff": mc, "rel_l2": (d.norm() / h_n.norm()).item(),
+                    "max_abs_err_over_max": (d.abs().max() / h_n.abs().max()).item(),
+                    "fwd_ms_numerical": t_n, "fwd_ms_analytic": t_b})
+    out = {"config": f"C4: {a.ng} Gaussians -> {a.hw}x{a.hw}x{a.t}, 32x32 angular, cuda preset, no occlusion",
+           "dr": dr, "s_min": s_min, "s_median": s_med,
+           "tolerance_rel_l2": (dr / s_min) ** 2 / 24, "expected_rel_l2_median": (dr / s_med) ** 2 / 24,
+           "results": res}
+    out["pass"] = all(r["rel_l2"] <= out["tolerance_rel_l2"] for r in res)
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
