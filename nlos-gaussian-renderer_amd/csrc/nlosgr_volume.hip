@@ -35,7 +35,23 @@
 using namespace nlosgr;
 using namespace nlosgr::detail;
 
+// A/B switches (compile-time; defaults are the production choice)
+#ifndef NLOSGR_FWD_PF
+#define NLOSGR_FWD_PF 0        // forward: prefetch the next Gaussian chunk into registers
+#endif
+#ifndef NLOSGR_FWD_WAVES
+#define NLOSGR_FWD_WAVES 6     // forward: minimum waves per SIMD the register allocation must allow
+#endif
+#ifndef NLOSGR_PACKED
+#define NLOSGR_PACKED 0        // packed fp32 (v_pk_*) in the backward drain (measured slower: 583 vs 564 ms)
+#endif
+#ifndef NLOSGR_BWD_PF
+#define NLOSGR_BWD_PF 0        // backward: prefetch the next wall point's gradient row / tables
+#endif
+
 namespace {
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 struct KArgs {
     nlosgr_gaussians g;
@@ -91,9 +107,10 @@ __device__ __forceinline__ void load_rec(const GaussRec& r, Pair& P, float mu[3]
     P.N[2] = r.e.x; P.N[3] = r.e.y; P.N[4] = r.e.z; P.N[5] = r.e.w;
 }
 
+// f: the Gaussian's feature row (k_feat floats; registers or global)
 template <int PRESET, bool DENSE>
-__device__ __forceinline__ void pair_setup(const KArgs& k, int gi, const float mu[3], float px, float py, float pz,
-                                           const float* lin, float mc2, Pair& P) {
+__device__ __forceinline__ void pair_setup(const KArgs& k, const float* f, const float mu[3], float px, float py,
+                                           float pz, const float* lin, float mc2, Pair& P) {
     P.q[0] = px - mu[0]; P.q[1] = py - mu[1]; P.q[2] = pz - mu[2];
     for (int r = 0; r < 3; ++r) P.u0[r] = P.A[3 * r] * P.q[0] + P.A[3 * r + 1] * P.q[1] + P.A[3 * r + 2] * P.q[2];
     view_dir<PRESET>(-P.q[0], -P.q[1], -P.q[2], P.dir[0], P.dir[1], P.dir[2], P.nrm);
@@ -101,7 +118,6 @@ __device__ __forceinline__ void pair_setup(const KArgs& k, int gi, const float m
     const int K = (deg + 1) * (deg + 1);
     float Y[kMaxK];
     sh_basis<PRESET>(deg, P.dir[0], P.dir[1], P.dir[2], Y);
-    const float* f = k.g.features + (size_t)gi * k.g.k_feat;
     float sh = 0.f;
 #pragma unroll
     for (int c = 0; c < kMaxK; ++c)
@@ -157,6 +173,22 @@ __device__ __forceinline__ void pair_setup(const KArgs& k, int gi, const float m
     }
 }
 
+// feature row -> registers (zero past k_feat)
+__device__ __forceinline__ void load_feat(const nlosgr_gaussians& g, int gi, float* f) {
+    const float* src = g.features + (size_t)gi * g.k_feat;
+    if (g.k_feat == kMaxK && (reinterpret_cast<uintptr_t>(g.features) & 15) == 0) {
+        const float4* s4 = reinterpret_cast<const float4*>(src);
+#pragma unroll
+        for (int c = 0; c < kMaxK / 4; ++c) {
+            const float4 v = s4[c];
+            f[4 * c] = v.x; f[4 * c + 1] = v.y; f[4 * c + 2] = v.z; f[4 * c + 3] = v.w;
+        }
+        return;
+    }
+#pragma unroll
+    for (int c = 0; c < kMaxK; ++c) f[c] = c < g.k_feat ? src[c] : 0.f;
+}
+
 __device__ __forceinline__ float quadric(const float* M, float dx, float dy, float dz) {
     const float t0 = fmaf(M[0], dx, fmaf(M[1], dy, M[2] * dz));
     const float t1 = fmaf(M[3], dy, M[4] * dz);
@@ -195,7 +227,11 @@ __device__ __forceinline__ bool ray_setup(const float* A, const float* u0, float
 // LDS carve helper (offsets in floats, 16-byte aligned)
 __host__ __device__ __forceinline__ int al4(int n) { return (n + 3) & ~3; }
 
-constexpr int kRQ = 128;      // ray queue capacity per wave (processed in batches of 64)
+#ifndef NLOSGR_RQ_SMALL
+#define NLOSGR_RQ_SMALL 0
+#endif
+// ray queue ring per wave: < 64 queued + up to 64 (small ring) or 128 appended per enumeration
+constexpr int kRQ = NLOSGR_RQ_SMALL ? 128 : 256;
 __device__ __forceinline__ unsigned pack_ray(int slot, int i, int j) {
     return (unsigned)slot | ((unsigned)i << 8) | ((unsigned)j << 20);
 }
@@ -209,8 +245,18 @@ __device__ __forceinline__ unsigned pack_ray(int slot, int i, int j) {
 // start bins differ — guaranteed per round by a claim table (owner[pos] = lane; losers retry
 // next round).  Lanes that did not win, or ran past their segment, point at private pad bins
 // and add 0, so the step body is branch-free.  Idle lanes are refilled from the ray queue.
-constexpr int kSteps = 16;     // bins per lane per drain round
-constexpr int kRefill = 24;    // refill once this many lanes are idle (or the queue is final)
+#ifndef NLOSGR_FSTEPS
+#define NLOSGR_FSTEPS 16
+#endif
+#ifndef NLOSGR_REFILL
+#define NLOSGR_REFILL 24
+#endif
+#ifndef NLOSGR_BREFILL
+#define NLOSGR_BREFILL 8
+#endif
+constexpr int kSteps = NLOSGR_FSTEPS;     // bins per lane per drain round
+constexpr int kRefill = NLOSGR_REFILL;    // refill once this many lanes are idle (or the queue is final)
+constexpr int kBRefill = NLOSGR_BREFILL;  // backward: same rule
 
 struct FwdLayout {
     int hist, owner, rayq, wave_stride, total;  // offsets in floats
@@ -270,59 +316,36 @@ __device__ __forceinline__ bool drain_setup(const float* A, const float* u0, flo
 }
 
 // Candidate enumeration (lane = pair): quadric test only; passing (pair, ray) entries are appended
-// to the ray queue ring at qbase + cnt.  Returns when cnt >= 64 or every lane exhausted its box.
-template <bool DENSE>
-__device__ __forceinline__ void enumerate_ring(const Pair& P, bool& more, int& ci, int& cj, const float2* tth,
-                                               const float2* tph, unsigned* rayq, int qbase, int& cnt) {
-    const int lane = lane_id();
-    while (__builtin_amdgcn_ballot_w64(more)) {
-        bool pass = false;
-        unsigned e = 0;
-        if (more) {
-            const float2 th = tth[ci], ph = tph[cj];
-            if (DENSE || quadric(P.M, th.x * ph.x, th.x * ph.y, th.y) >= 0.f) {
-                pass = true;
-                e = pack_ray(lane, ci, cj);
-            }
-            if (++cj > P.j1) { cj = P.j0; ++ci; }
-            more = ci <= P.i1;
-        }
-        const unsigned long long m = __builtin_amdgcn_ballot_w64(pass);
-        if (pass) rayq[(qbase + cnt + lanes_below(m)) & (kRQ - 1)] = e;
-        cnt += __popcll(m);
-        if (cnt >= 64) return;
-    }
-}
-
-// enumerate_ring over explicit quadric/box registers (backward: the pair state is not kept)
+// to the ray queue ring at qbase + cnt.  Branch-free body (every lane evaluates a clamped
+// candidate, `more` masks the result), two candidates per trip so their table reads overlap;
+// returns once cnt >= 64 or every lane exhausted its box (cnt < 64 + 2*64 <= kRQ on return).
 template <bool DENSE>
 __device__ __forceinline__ void enumerate_box(const float* M, int i1, int j0, int j1, bool& more, int& ci, int& cj,
-                                              const float2* tth, const float2* tph, unsigned* rayq, int qbase,
-                                              int& cnt) {
+                                              const float2* tth, const float2* tph, int nt1, unsigned* rayq,
+                                              int qbase, int& cnt) {
     const int lane = lane_id();
-    while (__builtin_amdgcn_ballot_w64(more)) {
-        bool pass = false;
-        unsigned e = 0;
-        if (more) {
-            const float2 th = tth[ci], ph = tph[cj];
-            if (DENSE || quadric(M, th.x * ph.x, th.x * ph.y, th.y) >= 0.f) {
-                pass = true;
-                e = pack_ray(lane, ci, cj);
-            }
-            if (++cj > j1) { cj = j0; ++ci; }
-            more = ci <= i1;
+    do {
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const float2 th = tth[min(ci, nt1)], ph = tph[cj];
+            const bool pass = more && (DENSE || quadric(M, th.x * ph.x, th.x * ph.y, th.y) >= 0.f);
+            const unsigned e = pack_ray(lane, ci, cj);
+            const bool wrap = cj >= j1;
+            cj = wrap ? j0 : cj + 1;
+            ci += wrap ? 1 : 0;
+            more = more && ci <= i1;
+            const unsigned long long m = __builtin_amdgcn_ballot_w64(pass);
+            if (pass) rayq[(qbase + cnt + lanes_below(m)) & (kRQ - 1)] = e;
+            cnt += __popcll(m);
+            if (NLOSGR_RQ_SMALL && cnt >= 64) return;
         }
-        const unsigned long long m = __builtin_amdgcn_ballot_w64(pass);
-        if (pass) rayq[(qbase + cnt + lanes_below(m)) & (kRQ - 1)] = e;
-        cnt += __popcll(m);
-        if (cnt >= 64) return;
-    }
+    } while (cnt < 64 && __builtin_amdgcn_ballot_w64(more));
 }
 
 __device__ __forceinline__ void compiler_fence() { __asm__ __volatile__("" ::: "memory"); }
 
 template <int PRESET, int MODE, bool DENSE, bool RAYS>
-__global__ __launch_bounds__(kBlock) void fwd_kernel(KArgs k) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_FWD_WAVES, 8))) void fwd_kernel(KArgs k) {
     extern __shared__ __align__(16) float smem[];
     const int nr = k.geo.nr, nt = k.geo.nt, np_ = k.geo.np;
     const FwdLayout L(nr, nt, np_);
@@ -364,6 +387,17 @@ __global__ __launch_bounds__(kBlock) void fwd_kernel(KArgs k) {
     bool act = false;
     int qhead = 0, qcount = 0;
 
+#if NLOSGR_FWD_PF
+    // the next chunk's Gaussian record and feature row are fetched into registers one chunk
+    // ahead, so their latency overlaps the current chunk's enumeration and drain
+    GaussRec nrec;
+    float nfeat[kMaxK];
+    {
+        const int g0 = min(wave * 64 + lane, k.g.ng - 1);
+        nrec = k.recs[g0];
+        load_feat(k.g, g0, nfeat);
+    }
+#endif
     for (int base = wave * 64;; base += kBlock) {
         const bool have = base < k.g.ng;      // wave-uniform
         Pair P;
@@ -373,10 +407,20 @@ __global__ __launch_bounds__(kBlock) void fwd_kernel(KArgs k) {
         P.i0 = P.i1 = P.j0 = P.j1 = 0;
         if (have) {
             const int gi = base + lane;
+#if !NLOSGR_FWD_PF
+            // all of the chunk's record and feature loads issued together, ahead of the setup math
+            GaussRec nrec;
+            float nfeat[kMaxK];
+            {
+                const int gl = min(gi, k.g.ng - 1);
+                nrec = k.recs[gl];
+                load_feat(k.g, gl, nfeat);
+            }
+#endif
             if (gi < k.g.ng) {
                 float mu[3];
-                load_rec(k.recs[gi], P, mu);
-                pair_setup<PRESET, DENSE>(k, gi, mu, px, py, pz, lin, mc2, P);
+                load_rec(nrec, P, mu);
+                pair_setup<PRESET, DENSE>(k, nfeat, mu, px, py, pz, lin, mc2, P);
                 more = (P.w > 0.f) && P.i0 <= P.i1 && P.j0 <= P.j1;
                 lw = more ? flog2(P.w) : 0.f;
                 sc = P.sigma * cdt;
@@ -385,11 +429,18 @@ __global__ __launch_bounds__(kBlock) void fwd_kernel(KArgs k) {
             if (flags & 2) more = false;      // diagnostics: pair setup only
             npair += __builtin_popcountll(__builtin_amdgcn_ballot_w64(more));
             ci = P.i0; cj = P.j0;
+#if NLOSGR_FWD_PF
+            if (base + kBlock < k.g.ng) {   // prefetch the next chunk
+                const int gn = min(base + kBlock + lane, k.g.ng - 1);
+                nrec = k.recs[gn];
+                load_feat(k.g, gn, nfeat);
+            }
+#endif
         }
         while (true) {
             if (qcount < 64 && __builtin_amdgcn_ballot_w64(more)) {
                 wave_sync();
-                enumerate_ring<DENSE>(P, more, ci, cj, tth, tph, rayq, qhead, qcount);
+                enumerate_box<DENSE>(P.M, P.i1, P.j0, P.j1, more, ci, cj, tth, tph, nt - 1, rayq, qhead, qcount);
                 wave_sync();
             }
             const bool anymore = __builtin_amdgcn_ballot_w64(more) != 0;
@@ -585,6 +636,45 @@ __device__ __forceinline__ void stage_grow(const float* grad, const float* att, 
     for (int t = nr + lane; t < nr + kBSteps; t += 64) grow[t] = 0.f;
 }
 
+// register prefetch of one wall point's backward inputs (see bwd_kernel)
+constexpr int kPFRow = 4;     // float4 per lane: rows up to 1024 bins
+struct RowPF {
+    float4 g[kPFRow];
+    float2 th, ph;
+    __device__ __forceinline__ void load(const KArgs& k, int p, int nr, int nt, int np_) {
+        const int lane = lane_id();
+        const float4* g4 = reinterpret_cast<const float4*>(k.grad_hist + (size_t)p * nr);
+        const int n4 = nr >> 2;
+#pragma unroll
+        for (int u = 0; u < kPFRow; ++u) {
+            const int t = lane + 64 * u;
+            g[u] = t < n4 ? g4[t] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        th = lane < nt ? make_float2(k.geo.sin_theta[(size_t)p * nt + lane], k.geo.cos_theta[(size_t)p * nt + lane])
+                       : make_float2(0.f, 0.f);
+        ph = lane < np_ ? make_float2(k.geo.cos_phi[(size_t)p * np_ + lane], k.geo.sin_phi[(size_t)p * np_ + lane])
+                        : make_float2(0.f, 0.f);
+    }
+    __device__ __forceinline__ void store(const float* att, float hs, int nr, int nt, int np_, float* grow,
+                                          float2* tth, float2* tph) const {
+        const int lane = lane_id();
+        const float4* a4 = reinterpret_cast<const float4*>(att);
+        const int n4 = nr >> 2;
+#pragma unroll
+        for (int u = 0; u < kPFRow; ++u) {
+            const int t = lane + 64 * u;
+            if (t < n4) {
+                const float4 a = a4[t];
+                reinterpret_cast<float4*>(grow)[t] =
+                    make_float4(g[u].x * a.x * hs, g[u].y * a.y * hs, g[u].z * a.z * hs, g[u].w * a.w * hs);
+            }
+        }
+        for (int t = nr + lane; t < nr + kBSteps; t += 64) grow[t] = 0.f;
+        if (lane < nt) tth[lane] = th;
+        if (lane < np_) tph[lane] = ph;
+    }
+};
+
 template <int MODE, bool DENSE>
 __device__ __forceinline__ bool bray_setup(const float* pd, float2 th, float2 ph, int slot, int i, int j, int nr,
                                            float mc2, float r0, float dr, float inv_dr, float f0log2, BRay& b) {
@@ -640,28 +730,42 @@ __global__ __launch_bounds__(kBlock) void bwd_kernel(KArgs k) {
     const float cdt = k.opt.c_deltaT;
     const float f0log2 = log2f(1.0f + 1e-7f);
     const float rscale = k.opt.ray_scale;
-    const float* fg = k.g.features + (size_t)(active ? gi : 0) * k.g.k_feat;
 
     float dA[9], dMu[3], dSig = 0.f, dF[kMaxK];
     for (int t = 0; t < 9; ++t) dA[t] = 0.f;
     dMu[0] = dMu[1] = dMu[2] = 0.f;
 #pragma unroll
     for (int t = 0; t < kMaxK; ++t) dF[t] = 0.f;
+    // this lane's Gaussian: record and feature row are re-read per wall point (L1/L2 hits) rather
+    // than held in registers across the split (VGPR budget)
+    const float* feat = k.g.features + (size_t)(active ? gi : 0) * k.g.k_feat;
     float mu[3] = {0.f, 0.f, 0.f};
     if (active) {
         const GaussRec rec = k.recs[gi];
         mu[0] = rec.a.x; mu[1] = rec.a.y; mu[2] = rec.a.z;
     }
 
+    // software pipeline over wall points: the next wall point's upstream gradient row and
+    // angle tables are loaded into registers while this one is processed (common shapes:
+    // nr <= 1024, nr % 4 == 0, nt, np <= 64); other shapes stage synchronously
+    const bool pf = NLOSGR_BWD_PF && k.grad_hist && nr <= 4 * 64 * kPFRow && (nr & 3) == 0 && nt <= 64 && np_ <= 64 &&
+                    ((reinterpret_cast<uintptr_t>(k.grad_hist) | reinterpret_cast<uintptr_t>(k.geo.att)) & 15) == 0;
+    RowPF rpf;
+    if (pf && pbeg + wave < pend) rpf.load(k, pbeg + wave, nr, nt, np_);
     for (int p = pbeg + wave; p < pend; p += kWaves) {
         // stage this wall point's upstream gradient row and tables (wave-private)
         const float hs = k.geo.hscale[p];
         wave_sync();
-        stage_grow(k.grad_hist ? k.grad_hist + (size_t)p * nr : nullptr, k.geo.att, hs, nr, grow);
-        for (int t = lane; t < nt; t += 64)
-            tth[t] = make_float2(k.geo.sin_theta[(size_t)p * nt + t], k.geo.cos_theta[(size_t)p * nt + t]);
-        for (int t = lane; t < np_; t += 64)
-            tph[t] = make_float2(k.geo.cos_phi[(size_t)p * np_ + t], k.geo.sin_phi[(size_t)p * np_ + t]);
+        if (pf) {
+            rpf.store(k.geo.att, hs, nr, nt, np_, grow, tth, tph);
+            if (p + kWaves < pend) rpf.load(k, p + kWaves, nr, nt, np_);
+        } else {
+            stage_grow(k.grad_hist ? k.grad_hist + (size_t)p * nr : nullptr, k.geo.att, hs, nr, grow);
+            for (int t = lane; t < nt; t += 64)
+                tth[t] = make_float2(k.geo.sin_theta[(size_t)p * nt + t], k.geo.cos_theta[(size_t)p * nt + t]);
+            for (int t = lane; t < np_; t += 64)
+                tph[t] = make_float2(k.geo.cos_phi[(size_t)p * np_ + t], k.geo.sin_phi[(size_t)p * np_ + t]);
+        }
         owner[lane] = 0xFFFFFFFFu;
         const float px = k.geo.wall[3 * p], py = k.geo.wall[3 * p + 1], pz = k.geo.wall[3 * p + 2];
         // pair setup (lane = Gaussian gi at wall point p); the ray pass reads the pair table
@@ -673,7 +777,7 @@ __global__ __launch_bounds__(kBlock) void bwd_kernel(KArgs k) {
             Pair P;
             float mu_[3];
             load_rec(k.recs[gi], P, mu_);
-            pair_setup<PRESET, DENSE>(k, gi, mu, px, py, pz, k.geo.grid_lin + 4 * (size_t)p, mc2, P);
+            pair_setup<PRESET, DENSE>(k, feat, mu, px, py, pz, k.geo.grid_lin + 4 * (size_t)p, mc2, P);
             more = (P.w > 0.f) && P.i0 <= P.i1 && P.j0 <= P.j1 && !(k.opt.flags & 2);  // flags 2: setup only
             for (int t = 0; t < 6; ++t) M[t] = P.M[t];
             i0 = P.i0; i1 = P.i1; j0 = P.j0; j1 = P.j1;
@@ -703,13 +807,13 @@ __global__ __launch_bounds__(kBlock) void bwd_kernel(KArgs k) {
         while (true) {
             if (qcount < 64 && __builtin_amdgcn_ballot_w64(more)) {
                 wave_sync();
-                enumerate_box<DENSE>(M, i1, j0, j1, more, ci, cj, tth, tph, rayq, qhead, qcount);
+                enumerate_box<DENSE>(M, i1, j0, j1, more, ci, cj, tth, tph, nt - 1, rayq, qhead, qcount);
                 wave_sync();
             }
             const bool anymore = __builtin_amdgcn_ballot_w64(more) != 0;
             const unsigned long long idle = __builtin_amdgcn_ballot_w64(!act && !pend);
             const int nidle = __popcll(idle);
-            if (qcount > 0 && (nidle >= kRefill || !anymore)) {
+            if (qcount > 0 && (nidle >= kBRefill || !anymore)) {
                 const int r = lanes_below(idle);
                 const bool take = !act && !pend && r < qcount;
                 if (take && !(k.opt.flags & 1)) {                  // flags 1: enumerate only
@@ -743,6 +847,24 @@ __global__ __launch_bounds__(kBlock) void bwd_kernel(KArgs k) {
                 }
                 float kap = b.kap;
                 if (MODE == NLOSGR_MODE_NOOCL) {
+#if NLOSGR_PACKED
+                    // two bins per instruction (v_pk_mul/fma/add_f32): even/odd partial sums
+                    f32x2 S0 = {b.S0, 0.f}, S1 = {b.S1, 0.f}, S2 = {b.S2, 0.f};
+                    f32x2 kv = {kap, kap + 1.f};
+                    const f32x2 c2 = {b.c2, b.c2}, c0 = {b.c0, b.c0};
+#pragma unroll
+                    for (int m = 0; m < kBSteps; m += 2) {
+                        const f32x2 e = kv * kv * c2 + c0;
+                        const f32x2 pv = {fast_exp2(e.x), fast_exp2(e.y)};
+                        const f32x2 H = {Hs[m], Hs[m + 1]};
+                        const f32x2 hp = H * pv;
+                        const f32x2 t1 = hp * kv;
+                        S0 += hp; S1 += t1; S2 += t1 * kv;
+                        kv += 2.f;
+                    }
+                    kap = kv.x;
+                    b.S0 = S0.x + S0.y; b.S1 = S1.x + S1.y; b.S2 = S2.x + S2.y;
+#else
                     float S0 = b.S0, S1 = b.S1, S2 = b.S2;
 #pragma unroll
                     for (int m = 0; m < kBSteps; ++m) {
@@ -752,6 +874,7 @@ __global__ __launch_bounds__(kBlock) void bwd_kernel(KArgs k) {
                         kap += 1.f;
                     }
                     b.S0 = S0; b.S1 = S1; b.S2 = S2;
+#endif
                 } else {
                     // dL/dD_j = c rho H_j T_j + (sum_{k>j} H_k out_k) f'_j / f_j  (two passes per ray)
                     float T = b.T, Etot = b.Etot, pre = b.pre;
@@ -860,7 +983,7 @@ __global__ __launch_bounds__(kBlock) void bwd_kernel(KArgs k) {
                 for (int cc = 0; cc < kMaxK; ++cc)
                     if (cc < K) dF[cc] += drho_pair * Y[cc];
                 float gx, gy, gz;
-                sh_grad_dir<PRESET>(deg, dir[0], dir[1], dir[2], fg, gx, gy, gz);
+                sh_grad_dir<PRESET>(deg, dir[0], dir[1], dir[2], feat, gx, gy, gz);
                 float ox, oy, oz;
                 view_dir_bwd<PRESET>(-q[0], -q[1], -q[2], nrm, drho_pair * gx, drho_pair * gy, drho_pair * gz, ox,
                                      oy, oz);
