@@ -131,7 +131,8 @@ def main():
     def step(timed):
         if timed:
             ev_fwd[0].record(stream)
-        hist, _ = render_forward(*params, geo, cfg, True, False)
+        # the forward records its in-support rays for the backward of the same step (ray cache)
+        hist, _, ws = render_forward(*params, geo, cfg, True, False, ray_cache=not fwd_only)
         if timed:
             ev_fwd[1].record(stream)
         if fwd_only:
@@ -140,7 +141,7 @@ def main():
         grad = (2.0 / hist.numel()) * (hist - target)
         if timed:
             ev_bwd[0].record(stream)
-        grads = render_backward(*params, geo, cfg, grad_hist=grad)
+        grads = render_backward(*params, geo, cfg, grad_hist=grad, workspace=ws, ray_cache=True)
         if timed:
             ev_bwd[1].record(stream)
         if world > 1:

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define NLOSGR_ABI_VERSION 1
+#define NLOSGR_ABI_VERSION 2
 
 /* convention presets */
 enum {
@@ -98,10 +98,16 @@ typedef struct {
     float c_deltaT;           /* c * deltaT (netf transmittance) */
     float ray_scale;          /* scale applied to the optional per-ray output (e.g. c*dT) */
     int32_t nsplit;           /* backward: wall-point splits (0 -> auto) */
-    int32_t flags;            /* reserved, 0 */
+    int32_t flags;            /* diagnostics only (phase ablation), 0 */
+    int32_t ray_cache;        /* 1: the forward records, per (wall point, Gaussian) pair, which rays
+                                 of its candidate box are in support (20 B per pair in the workspace,
+                                 see nlosgr_workspace_bytes) and a backward on the SAME workspace with
+                                 the SAME inputs walks that record instead of re-testing the rays.
+                                 Culled (cutoff > 0), histogram-only calls; 0 = off */
 } nlosgr_options;
 
-/* Scratch bytes needed by fwd/bwd for this problem (caller allocates, 256-B aligned). */
+/* Scratch bytes needed by fwd/bwd for this problem (caller allocates, 256-B aligned); includes
+ * nwall*ng*20 B for the ray cache when opt->ray_cache is set. */
 NLOSGR_API size_t nlosgr_workspace_bytes(const nlosgr_gaussians* g, const nlosgr_geometry* geo,
                               const nlosgr_options* opt);
 

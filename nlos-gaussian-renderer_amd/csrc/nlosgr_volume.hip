@@ -45,6 +45,12 @@ using namespace nlosgr::detail;
 #ifndef NLOSGR_PACKED
 #define NLOSGR_PACKED 0        // packed fp32 (v_pk_*) in the backward drain (measured slower: 583 vs 564 ms)
 #endif
+#ifndef NLOSGR_BWD_WAVES
+#define NLOSGR_BWD_WAVES 4     // backward: minimum waves per SIMD (4: 470 -> 444 ms at C3, few spills)
+#endif
+#ifndef NLOSGR_FPACKED
+#define NLOSGR_FPACKED 0       // packed fp32 (v_pk_*) in the forward drain
+#endif
 #ifndef NLOSGR_BWD_PF
 #define NLOSGR_BWD_PF 0        // backward: prefetch the next wall point's gradient row / tables
 #endif
@@ -65,7 +71,17 @@ struct KArgs {
     float* partial;  // [nsplit][ng][32]
     int nsplit;
     unsigned long long* counts;  // optional [3]: pairs, segments, samples (nlosgr_count_support)
+    ulonglong2* cmask;           // ray cache [P][ng]: passing rays of the pair's box (bit = box cell)
+    unsigned* cbox;              // ray cache [P][ng]: i0 | j0 << 12 | width << 24, 0 = not cached
 };
+
+// ray cache: a pair whose (theta, phi) candidate box has at most 128 cells records which cells
+// passed the quadric test in the forward; the backward walks those bits instead of re-testing
+// (C3: 99.9% of pairs; the rest are re-enumerated)
+constexpr int kCacheCells = 128;
+__device__ __forceinline__ unsigned cache_box(int i0, int j0, int w) {
+    return (unsigned)i0 | ((unsigned)j0 << 12) | ((unsigned)w << 24);
+}
 
 // atan2 with |error| < 2e-6 rad (minimax on [0,1] + octant reduction); used only for the
 // conservative footprint box, which is widened by kAngMargin.
@@ -319,16 +335,23 @@ __device__ __forceinline__ bool drain_setup(const float* A, const float* u0, flo
 // to the ray queue ring at qbase + cnt.  Branch-free body (every lane evaluates a clamped
 // candidate, `more` masks the result), two candidates per trip so their table reads overlap;
 // returns once cnt >= 64 or every lane exhausted its box (cnt < 64 + 2*64 <= kRQ on return).
-template <bool DENSE>
+template <bool DENSE, bool REC = false>
 __device__ __forceinline__ void enumerate_box(const float* M, int i1, int j0, int j1, bool& more, int& ci, int& cj,
                                               const float2* tth, const float2* tph, int nt1, unsigned* rayq,
-                                              int qbase, int& cnt) {
+                                              int qbase, int& cnt, unsigned long long* rec0 = nullptr,
+                                              unsigned long long* rec1 = nullptr, int* cell = nullptr) {
     const int lane = lane_id();
     do {
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
             const float2 th = tth[min(ci, nt1)], ph = tph[cj];
             const bool pass = more && (DENSE || quadric(M, th.x * ph.x, th.x * ph.y, th.y) >= 0.f);
+            if (REC) {   // cell index within the box (only boxes of <= 128 cells are cached)
+                const unsigned long long bit = 1ull << (*cell & 63);
+                *rec0 |= (pass && *cell < 64) ? bit : 0ull;
+                *rec1 |= (pass && (*cell >> 6) == 1) ? bit : 0ull;
+                *cell += 1;
+            }
             const unsigned e = pack_ray(lane, ci, cj);
             const bool wrap = cj >= j1;
             cj = wrap ? j0 : cj + 1;
@@ -342,9 +365,31 @@ __device__ __forceinline__ void enumerate_box(const float* M, int i1, int j0, in
     } while (cnt < 64 && __builtin_amdgcn_ballot_w64(more));
 }
 
+// Ray-cache walk (backward): each lane pops the lowest set cell of its pair's cached mask and
+// appends that ray; same queue discipline as enumerate_box (no quadric, no table reads).
+__device__ __forceinline__ void enumerate_cached(unsigned long long& bits0, unsigned long long& bits1, int ci0,
+                                                 int cj0, int cw, float rcw, unsigned* rayq, int qbase, int& cnt) {
+    const int lane = lane_id();
+    do {
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const bool lo = bits0 != 0ull;
+            const bool pass = lo || bits1 != 0ull;
+            const int b = lo ? (int)__builtin_ctzll(bits0) : (pass ? 64 + (int)__builtin_ctzll(bits1) : 0);
+            if (lo) bits0 &= bits0 - 1ull;
+            else bits1 &= bits1 - 1ull;
+            const int di = (int)(((float)b + 0.5f) * rcw);
+            const unsigned e = pack_ray(lane, ci0 + di, cj0 + b - di * cw);
+            const unsigned long long m = __builtin_amdgcn_ballot_w64(pass);
+            if (pass) rayq[(qbase + cnt + lanes_below(m)) & (kRQ - 1)] = e;
+            cnt += __popcll(m);
+        }
+    } while (cnt < 64 && __builtin_amdgcn_ballot_w64((bits0 | bits1) != 0ull));
+}
+
 __device__ __forceinline__ void compiler_fence() { __asm__ __volatile__("" ::: "memory"); }
 
-template <int PRESET, int MODE, bool DENSE, bool RAYS>
+template <int PRESET, int MODE, bool DENSE, bool RAYS, bool CACHE>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_FWD_WAVES, 8))) void fwd_kernel(KArgs k) {
     extern __shared__ __align__(16) float smem[];
     const int nr = k.geo.nr, nt = k.geo.nt, np_ = k.geo.np;
@@ -404,6 +449,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_F
         float lw = 0.f, sc = 0.f, lwc = 0.f;
         bool more = false;
         int ci = 0, cj = 0;
+        unsigned long long crec0 = 0ull, crec1 = 0ull;   // CACHE: passing cells of this lane's box
+        int ccell = 0;
         P.i0 = P.i1 = P.j0 = P.j1 = 0;
         if (have) {
             const int gi = base + lane;
@@ -440,7 +487,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_F
         while (true) {
             if (qcount < 64 && __builtin_amdgcn_ballot_w64(more)) {
                 wave_sync();
-                enumerate_box<DENSE>(P.M, P.i1, P.j0, P.j1, more, ci, cj, tth, tph, nt - 1, rayq, qhead, qcount);
+                enumerate_box<DENSE, CACHE>(P.M, P.i1, P.j0, P.j1, more, ci, cj, tth, tph, nt - 1, rayq, qhead,
+                                            qcount, &crec0, &crec1, &ccell);
                 wave_sync();
             }
             const bool anymore = __builtin_amdgcn_ballot_w64(more) != 0;
@@ -488,6 +536,25 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_F
             float t = d.t;
             float logT = d.logT;
             float xlo = d.xlo, elo = d.elo;
+            if (NLOSGR_FPACKED && MODE == NLOSGR_MODE_NOOCL && !RAYS) {
+                // two bins per v_pk_mul/v_pk_fma/v_pk_add; the LDS read-add-write stays in bin order
+                f32x2 tv = {t, t + 1.f};
+                const f32x2 gav = {d.ga, d.ga}, alv = {d.al, d.al};
+#pragma unroll
+                for (int m = 0; m < kSteps; m += 2) {
+                    const f32x2 e = tv * tv * gav + alv;
+                    const float v0 = m < remw ? fast_exp2(e.x) : 0.f;
+                    const float v1 = m + 1 < remw ? fast_exp2(e.y) : 0.f;
+                    const float x0 = hb[m];
+                    hb[m] = x0 + v0;
+                    compiler_fence();
+                    const float x1 = hb[m + 1];
+                    hb[m + 1] = x1 + v1;
+                    compiler_fence();
+                    tv += 2.f;
+                }
+                t = tv.x;
+            } else
 #pragma unroll
             for (int m = 0; m < kSteps; ++m) {
                 const bool in = m < remw;
@@ -535,6 +602,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_F
                 d.rem -= kSteps;
                 act = d.rem > 0;
             }
+        }
+        if (CACHE && have && base + lane < k.g.ng) {
+            // every candidate of this chunk has been tested: record the pair's passing cells
+            const int bw = P.j1 - P.j0 + 1, bh = P.i1 - P.i0 + 1;
+            const bool live = P.w > 0.f && bw > 0 && bh > 0;
+            const size_t o = (size_t)p * k.g.ng + base + lane;
+            const bool ok = !live || bw * bh <= kCacheCells;
+            k.cmask[o] = live ? make_ulonglong2(crec0, crec1) : make_ulonglong2(0ull, 0ull);
+            k.cbox[o] = ok ? cache_box(live ? P.i0 : 0, live ? P.j0 : 0, live ? bw : 1) : 0u;
         }
         if (!have) break;
     }
@@ -701,8 +777,8 @@ __device__ __forceinline__ bool bray_setup(const float* pd, float2 th, float2 ph
     return true;
 }
 
-template <int PRESET, int MODE, bool DENSE, bool RAYS>
-__global__ __launch_bounds__(kBlock) void bwd_kernel(KArgs k) {
+template <int PRESET, int MODE, bool DENSE, bool RAYS, bool CACHE>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_BWD_WAVES, 8))) void bwd_kernel(KArgs k) {
     extern __shared__ __align__(16) float smem[];
     const int nr = k.geo.nr, nt = k.geo.nt, np_ = k.geo.np, P_ = k.geo.nwall;
     const BwdLayout L(nr, nt, np_);
@@ -788,6 +864,22 @@ __global__ __launch_bounds__(kBlock) void bwd_kernel(KArgs k) {
             d4[2] = make_float4(P.A[8], P.u0[0], P.u0[1], P.u0[2]);
             d4[3] = make_float4(P.w, P.rho, P.sigma, 0.f);
         }
+        // ray cache of the forward: cached pairs walk their recorded cells instead of enumerating
+        unsigned long long cbits0 = 0ull, cbits1 = 0ull;
+        int ci0 = 0, cj0 = 0, cw = 1;
+        float rcw = 1.f;
+        if (CACHE && active) {
+            const size_t o = (size_t)p * k.g.ng + gi;
+            const unsigned bx = k.cbox[o];
+            if (bx != 0u) {
+                const ulonglong2 cm = k.cmask[o];
+                cbits0 = more ? cm.x : 0ull;
+                cbits1 = more ? cm.y : 0ull;
+                ci0 = bx & 0xFFF; cj0 = (bx >> 12) & 0xFFF; cw = bx >> 24;
+                rcw = 1.0f / (float)cw;
+                more = false;
+            }
+        }
         const float* gray = RAYS && k.grad_ray ? k.grad_ray + (size_t)p * nt * np_ * nr : nullptr;
         wave_sync();
         int ci = i0, cj = j0, qhead = 0, qcount = 0;
@@ -805,12 +897,17 @@ __global__ __launch_bounds__(kBlock) void bwd_kernel(KArgs k) {
         // pending result of a finished ray: dL/du0, dL/dv, dsigma, drho
         float rU[3] = {0.f, 0.f, 0.f}, rV[3] = {0.f, 0.f, 0.f}, rSig = 0.f, rRho = 0.f;
         while (true) {
+            if (CACHE && qcount < 64 && __builtin_amdgcn_ballot_w64((cbits0 | cbits1) != 0ull)) {
+                wave_sync();
+                enumerate_cached(cbits0, cbits1, ci0, cj0, cw, rcw, rayq, qhead, qcount);
+                wave_sync();
+            }
             if (qcount < 64 && __builtin_amdgcn_ballot_w64(more)) {
                 wave_sync();
                 enumerate_box<DENSE>(M, i1, j0, j1, more, ci, cj, tth, tph, nt - 1, rayq, qhead, qcount);
                 wave_sync();
             }
-            const bool anymore = __builtin_amdgcn_ballot_w64(more) != 0;
+            const bool anymore = __builtin_amdgcn_ballot_w64(more || (CACHE && (cbits0 | cbits1) != 0ull)) != 0;
             const unsigned long long idle = __builtin_amdgcn_ballot_w64(!act && !pend);
             const int nidle = __popcll(idle);
             if (qcount > 0 && (nidle >= kBRefill || !anymore)) {
@@ -1111,37 +1208,53 @@ int bwd_nsplit(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlos
 }
 
 
-template <int PRESET, int MODE, bool DENSE, bool RAYS>
+template <int PRESET, int MODE, bool DENSE, bool RAYS, bool CACHE>
 void launch_fwd(const KArgs& ka, size_t shm, hipStream_t s) {
-    hipLaunchKernelGGL((fwd_kernel<PRESET, MODE, DENSE, RAYS>), dim3(ka.geo.nwall), dim3(kBlock), shm, s, ka);
+    hipLaunchKernelGGL((fwd_kernel<PRESET, MODE, DENSE, RAYS, CACHE>), dim3(ka.geo.nwall), dim3(kBlock), shm, s, ka);
 }
-template <int PRESET, int MODE, bool DENSE, bool RAYS>
+template <int PRESET, int MODE, bool DENSE, bool RAYS, bool CACHE>
 void launch_bwd(const KArgs& ka, size_t shm, hipStream_t s) {
     dim3 grid((ka.g.ng + kNB - 1) / kNB, ka.nsplit);
-    hipLaunchKernelGGL((bwd_kernel<PRESET, MODE, DENSE, RAYS>), grid, dim3(kBlock), shm, s, ka);
+    hipLaunchKernelGGL((bwd_kernel<PRESET, MODE, DENSE, RAYS, CACHE>), grid, dim3(kBlock), shm, s, ka);
 }
 
+// the ray cache is used only by the culled, histogram-only variants (the training hot path)
 template <int PRESET, int MODE>
 void dispatch_fwd(const KArgs& ka, bool dense, bool rays, size_t shm, hipStream_t s) {
     if (dense) {
-        if (rays) launch_fwd<PRESET, MODE, true, true>(ka, shm, s);
-        else launch_fwd<PRESET, MODE, true, false>(ka, shm, s);
+        if (rays) launch_fwd<PRESET, MODE, true, true, false>(ka, shm, s);
+        else launch_fwd<PRESET, MODE, true, false, false>(ka, shm, s);
     } else {
-        if (rays) launch_fwd<PRESET, MODE, false, true>(ka, shm, s);
-        else launch_fwd<PRESET, MODE, false, false>(ka, shm, s);
+        if (rays) launch_fwd<PRESET, MODE, false, true, false>(ka, shm, s);
+        else if (ka.cmask && MODE != NLOSGR_MODE_BININT) launch_fwd<PRESET, MODE, false, false, MODE != NLOSGR_MODE_BININT>(ka, shm, s);
+        else launch_fwd<PRESET, MODE, false, false, false>(ka, shm, s);
     }
 }
 template <int PRESET, int MODE>
 void dispatch_bwd(const KArgs& ka, bool dense, bool rays, size_t shm, hipStream_t s) {
     if (dense) {
-        if (rays) launch_bwd<PRESET, MODE, true, true>(ka, shm, s);
-        else launch_bwd<PRESET, MODE, true, false>(ka, shm, s);
+        if (rays) launch_bwd<PRESET, MODE, true, true, false>(ka, shm, s);
+        else launch_bwd<PRESET, MODE, true, false, false>(ka, shm, s);
     } else {
-        if (rays) launch_bwd<PRESET, MODE, false, true>(ka, shm, s);
-        else launch_bwd<PRESET, MODE, false, false>(ka, shm, s);
+        if (rays) launch_bwd<PRESET, MODE, false, true, false>(ka, shm, s);
+        else if (ka.cmask) launch_bwd<PRESET, MODE, false, false, true>(ka, shm, s);
+        else launch_bwd<PRESET, MODE, false, false, false>(ka, shm, s);
     }
 }
 
+
+// workspace layout: GaussRec[ng] | backward partials [nsplit][ng][32] | ray cache (opt->ray_cache):
+// mask 2 x u64 [P][ng] | box u32 [P][ng]
+size_t cache_bytes(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_options* opt) {
+    return opt->ray_cache ? align_up((size_t)geo->nwall * g->ng * 20) : 0;
+}
+void cache_ptrs(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_options* opt, void* ws, int nsplit,
+                KArgs& ka) {
+    if (!opt->ray_cache || g->ng == 0 || geo->nwall == 0) return;
+    char* base = (char*)ws + align_up((size_t)g->ng * sizeof(GaussRec)) + align_up((size_t)nsplit * g->ng * 32 * sizeof(float));
+    ka.cmask = (ulonglong2*)base;
+    ka.cbox = (unsigned*)(base + (size_t)geo->nwall * g->ng * 16);
+}
 
 int run_fwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_options* opt, void* workspace,
             float* hist_out, float* ray_out, unsigned long long* counts, hipStream_t s) {
@@ -1152,6 +1265,7 @@ int run_fwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_
     ka.recs = (const GaussRec*)workspace;
     ka.hist_out = hist_out; ka.ray_out = ray_out;
     ka.counts = counts;
+    if (!counts) cache_ptrs(g, geo, opt, workspace, bwd_nsplit(g, geo, opt), ka);
     if (g->ng > 0) {
         launch_preprocess(g, (GaussRec*)workspace, s);
         HIPCHK(hipGetLastError());
@@ -1184,7 +1298,7 @@ size_t nlosgr_workspace_bytes(const nlosgr_gaussians* g, const nlosgr_geometry* 
     if (validate(g, geo, opt) != NLOSGR_OK) return 0;
     const size_t rec = align_up((size_t)g->ng * sizeof(GaussRec));
     const size_t part = align_up((size_t)bwd_nsplit(g, geo, opt) * g->ng * 32 * sizeof(float));
-    return rec + part + 256;
+    return rec + part + cache_bytes(g, geo, opt) + 256;
 }
 
 int nlosgr_render_fwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_options* opt,
@@ -1226,6 +1340,7 @@ int nlosgr_render_bwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo, con
     ka.partial = (float*)((char*)workspace + align_up((size_t)g->ng * sizeof(GaussRec)));
     ka.grad_hist = grad_hist; ka.grad_ray = grad_ray;
     ka.nsplit = bwd_nsplit(g, geo, opt);
+    cache_ptrs(g, geo, opt, workspace, ka.nsplit, ka);
     launch_preprocess(g, (GaussRec*)workspace, s);
     HIPCHK(hipGetLastError());
     if (geo->nwall > 0 && (grad_hist || grad_ray)) {

@@ -38,7 +38,8 @@ class Geometry(ctypes.Structure):
 
 class Options(ctypes.Structure):
     _fields_ = [("mode", ctypes.c_int32), ("cutoff", ctypes.c_float), ("c_deltaT", ctypes.c_float),
-                ("ray_scale", ctypes.c_float), ("nsplit", ctypes.c_int32), ("flags", ctypes.c_int32)]
+                ("ray_scale", ctypes.c_float), ("nsplit", ctypes.c_int32), ("flags", ctypes.c_int32),
+                ("ray_cache", ctypes.c_int32)]
 
 
 class Rays(ctypes.Structure):
@@ -47,6 +48,7 @@ class Rays(ctypes.Structure):
 
 
 MAX_PER_RAY = 256   # NLOSGR_MAX_PER_RAY
+ABI_VERSION = 2     # NLOSGR_ABI_VERSION
 
 # every symbol include/nlosgr.h declares (tests check the exports against this list)
 EXPORTS = ["nlosgr_workspace_bytes", "nlosgr_render_fwd", "nlosgr_render_bwd", "nlosgr_count_support",
@@ -93,7 +95,7 @@ def load():
     lib.nlosgr_last_error.restype = ctypes.c_char_p
     lib.nlosgr_abi_version.argtypes = []
     lib.nlosgr_abi_version.restype = ctypes.c_int
-    if lib.nlosgr_abi_version() != 1:
+    if lib.nlosgr_abi_version() != ABI_VERSION:
         raise RuntimeError("nlosgr: ABI version mismatch")
     _lib = lib
     return lib

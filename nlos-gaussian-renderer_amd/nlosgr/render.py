@@ -8,11 +8,15 @@ the batched volume renderer, the multi-GPU shard) is built on.  It returns
 and backward yields real gradients for the five raw parameter tensors (the reference's
 CUDA backward returns zeros, gaussian_model/cuda_autograd.py:147-156).
 """
+import os
 from dataclasses import dataclass
 
 import torch
 
 from . import _lib
+
+# upper bound on the forward->backward ray cache (20 B per wall point x Gaussian pair; C3: 33 GB)
+RAY_CACHE_MAX_BYTES = int(float(os.environ.get("NLOSGR_RAY_CACHE_GB", "96")) * 2 ** 30)
 
 
 @dataclass(frozen=True)
@@ -26,6 +30,13 @@ class RenderConfig:
     ray_scale: float = 1.0
     nsplit: int = 0
     flags: int = 0               # ablation / diagnostics only (0 in production)
+    ray_cache: bool = True       # forward records in-support rays per pair for the backward
+
+
+def use_ray_cache(cfg, geo, ng, want_rays=False):
+    """The forward->backward ray cache applies to culled, histogram-only, differentiable modes."""
+    return (bool(cfg.ray_cache) and cfg.cutoff > 0 and not want_rays and cfg.mode in ("noocl", "netf")
+            and geo.nwall * ng * 20 <= RAY_CACHE_MAX_BYTES)
 
 
 def _as_f32(t):
@@ -37,7 +48,7 @@ def _as_f32(t):
     return t.contiguous()
 
 
-def _structs(mu, scaling, rotation, opacity, features, geo, cfg):
+def _structs(mu, scaling, rotation, opacity, features, geo, cfg, ray_cache=False):
     ng = mu.shape[0]
     k_feat = features.shape[1] if features.dim() == 2 else 0
     if mu.shape != (ng, 3) or scaling.shape != (ng, 3) or rotation.shape != (ng, 4):
@@ -51,7 +62,7 @@ def _structs(mu, scaling, rotation, opacity, features, geo, cfg):
                        _lib.ptr(geo.cos_theta), _lib.ptr(geo.sin_phi), _lib.ptr(geo.cos_phi),
                        _lib.ptr(geo.grid_lin), _lib.ptr(geo.hscale), _lib.ptr(geo.r), _lib.ptr(geo.att))
     o = _lib.Options(_lib.MODES[cfg.mode], float(cfg.cutoff), float(cfg.c_deltaT), float(cfg.ray_scale),
-                     int(cfg.nsplit), int(cfg.flags))
+                     int(cfg.nsplit), int(cfg.flags), int(bool(ray_cache)))
     return g, gs, o
 
 
@@ -62,26 +73,36 @@ def _workspace(lib, g, gs, o, device):
     return torch.empty(nbytes, dtype=torch.uint8, device=device)
 
 
-def render_forward(mu, scaling, rotation, opacity, features, geo, cfg, want_hist=True, want_rays=False):
-    """Non-differentiable forward (used by RenderFn and by inference callers)."""
+def render_forward(mu, scaling, rotation, opacity, features, geo, cfg, want_hist=True, want_rays=False,
+                   workspace=None, ray_cache=False):
+    """Non-differentiable forward (used by RenderFn and by inference callers).  With ray_cache the
+    forward records its in-support rays in `workspace` (which must then be passed, unchanged, to
+    the backward of the same inputs); returns (hist, rays) or, with ray_cache, (hist, rays, ws)."""
     lib = _lib.load()
     dev = mu.device
     mu, scaling, rotation, opacity, features = [_as_f32(t) for t in (mu, scaling, rotation, opacity, features)]
-    g, gs, o = _structs(mu, scaling, rotation, opacity, features, geo, cfg)
-    ws = _workspace(lib, g, gs, o, dev)
+    g, gs, o = _structs(mu, scaling, rotation, opacity, features, geo, cfg, ray_cache)
+    ws = _workspace(lib, g, gs, o, dev) if workspace is None else workspace
     hist = torch.empty(geo.nwall, geo.nr, device=dev) if want_hist else None
     rays = torch.zeros(geo.nwall, geo.nt * geo.np, geo.nr, device=dev) if want_rays else None
     _lib.check(lib.nlosgr_render_fwd(g, gs, o, _lib.ptr(ws), _lib.ptr(hist), _lib.ptr(rays),
                                      _lib.stream_handle(dev)))
+    if ray_cache:
+        return hist, rays, ws
     return hist, rays
 
 
-def render_backward(mu, scaling, rotation, opacity, features, geo, cfg, grad_hist=None, grad_rays=None):
+def render_backward(mu, scaling, rotation, opacity, features, geo, cfg, grad_hist=None, grad_rays=None,
+                    workspace=None, ray_cache=False):
+    """Gradients of the five raw parameter tensors.  ray_cache: `workspace` holds the ray record of
+    a forward of the same inputs (render_forward(..., ray_cache=True))."""
     lib = _lib.load()
     dev = mu.device
     mu, scaling, rotation, opacity, features = [_as_f32(t) for t in (mu, scaling, rotation, opacity, features)]
-    g, gs, o = _structs(mu, scaling, rotation, opacity, features, geo, cfg)
-    ws = _workspace(lib, g, gs, o, dev)
+    g, gs, o = _structs(mu, scaling, rotation, opacity, features, geo, cfg, ray_cache)
+    if ray_cache and workspace is None:
+        raise ValueError("nlosgr: ray_cache backward needs the forward's workspace")
+    ws = _workspace(lib, g, gs, o, dev) if workspace is None else workspace
     gh = grad_hist.float().contiguous() if grad_hist is not None else None
     gr = grad_rays.float().contiguous() if grad_rays is not None else None
     d_mu = torch.empty_like(mu)
@@ -111,7 +132,11 @@ def count_support(mu, scaling, rotation, opacity, features, geo, cfg):
 class RenderFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, mu, scaling, rotation, opacity, features, geo, cfg, want_hist, want_rays):
-        hist, rays = render_forward(mu, scaling, rotation, opacity, features, geo, cfg, want_hist, want_rays)
+        cache = use_ray_cache(cfg, geo, mu.shape[0], want_rays) and any(ctx.needs_input_grad[:5])
+        out = render_forward(mu, scaling, rotation, opacity, features, geo, cfg, want_hist, want_rays,
+                             ray_cache=cache)
+        hist, rays = out[0], out[1]
+        ctx.ws = out[2] if cache else None     # the ray record lives until the backward
         ctx.save_for_backward(mu, scaling, rotation, opacity, features)
         ctx.geo, ctx.cfg, ctx.oshape = geo, cfg, opacity.shape
         outs = (hist if hist is not None else torch.zeros(0, device=mu.device),
@@ -124,7 +149,8 @@ class RenderFn(torch.autograd.Function):
         gh = g_hist if (g_hist is not None and g_hist.numel() > 0) else None
         gr = g_rays if (g_rays is not None and g_rays.numel() > 0) else None
         d_mu, d_s, d_q, d_o, d_f = render_backward(mu, scaling, rotation, opacity, features, ctx.geo, ctx.cfg,
-                                                   gh, gr)
+                                                   gh, gr, workspace=ctx.ws, ray_cache=ctx.ws is not None)
+        ctx.ws = None
         return d_mu, d_s, d_q, d_o.reshape(ctx.oshape), d_f, None, None, None, None
 
 

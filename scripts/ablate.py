@@ -23,12 +23,14 @@ for flags in (0, 4, 1, 2):
     render_forward(*args, cfg); torch.cuda.synchronize()
     t0 = time.perf_counter(); render_forward(*args, cfg); torch.cuda.synchronize()
     res[flags] = (time.perf_counter() - t0) * 1000
-hist, _ = render_forward(*args, base)
+cache = os.environ.get("NLOSGR_ABLATE_CACHE", "1") == "1"
+hist, _, ws = render_forward(*args, base, ray_cache=True)
 grad = torch.randn_like(hist) * 1e-3
 bres = {}
 for flags in (0, 4, 1, 2):
     cfg = dataclasses.replace(base, flags=flags)
-    render_backward(*args, cfg, grad_hist=grad); torch.cuda.synchronize()
-    t0 = time.perf_counter(); render_backward(*args, cfg, grad_hist=grad); torch.cuda.synchronize()
+    kw = dict(workspace=ws, ray_cache=True) if cache else {}
+    render_backward(*args, cfg, grad_hist=grad, **kw); torch.cuda.synchronize()
+    t0 = time.perf_counter(); render_backward(*args, cfg, grad_hist=grad, **kw); torch.cuda.synchronize()
     bres[flags] = (time.perf_counter() - t0) * 1000
-print(json.dumps({'config': cfgname, 'fwd_ms_by_flags': res, 'bwd_ms_by_flags': bres}))
+print(json.dumps({'config': cfgname, 'ray_cache': cache, 'fwd_ms_by_flags': res, 'bwd_ms_by_flags': bres}))

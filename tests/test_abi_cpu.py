@@ -23,7 +23,7 @@ def test_library_exports_header_symbols():
     assert sorted(_lib.EXPORTS) == syms
     for s in syms:
         assert hasattr(lib, s), s
-    assert lib.nlosgr_abi_version() == 1
+    assert lib.nlosgr_abi_version() == _lib.ABI_VERSION
 
 
 def test_validation_errors_without_gpu():

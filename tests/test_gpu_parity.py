@@ -169,3 +169,30 @@ def test_count_support_vs_oracle(preset):
     ref = R.count_support(P, cpu(walls), cpu(box), ns, start, end, c, deltaT, preset, mc)
     # boundary samples (m2 within fp32 rounding of mc^2) may flip
     assert abs(evals - ref) <= max(2, 1e-3 * ref), (evals, ref)
+
+
+@pytest.mark.parametrize("mode", ["noocl", "netf"])
+def test_ray_cache_backward_matches_uncached(mode):
+    """The forward's ray record (ray_cache) changes only the order in which the backward visits
+    rays: gradients equal the uncached backward within fp32 summation-order noise, and the
+    forward output is unchanged."""
+    from nlosgr import GaussianParams, features_flat
+    from nlosgr.volume import Scene, make_config
+    from nlosgr.render import render_backward, render_forward
+    dev = torch.device("cuda:0")
+    scene = Scene(H=6, W=5, T=256, ns=16)
+    m = GaussianParams.synthetic(3000, 3, preset="cuda", device=dev, seed=4)
+    with torch.no_grad():
+        m._scaling.add_(0.4)       # boxes of more than 64 cells for some pairs (uncached fallback)
+    geo = scene.geometry(dev, "cuda", mode)
+    cfg = make_config(m, scene, mode=mode, cutoff=3.0)
+    args = (m._mu.detach(), m._scaling.detach(), m._rotation.detach(), m._opacity.detach(),
+            features_flat(m).detach().contiguous(), geo)
+    h0, _ = render_forward(*args, cfg)
+    h1, _, ws = render_forward(*args, cfg, ray_cache=True)
+    assert torch.equal(h0, h1)
+    g = torch.randn(h0.shape, generator=torch.Generator().manual_seed(3)).to(dev) * 1e-3
+    ref = render_backward(*args, cfg, grad_hist=g)
+    got = render_backward(*args, cfg, grad_hist=g, workspace=ws, ray_cache=True)
+    for name, a, b in zip(["mu", "scaling", "rotation", "opacity", "features"], got, ref):
+        _close(a.cpu(), b.cpu(), 1e-5, 1e-9, f"cached grad {name}")
