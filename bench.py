@@ -1,9 +1,10 @@
 """Benchmark: transient volumes/sec (fwd+bwd), 100k Gaussians -> 128x128x1024 ToF bins (BASELINE.json).
 
 One step = render the whole 128x128-wall-point x 1024-bin transient volume (32x32 angular
-samples per wall point, "cuda" preset, no occlusion), MSE against a target volume, backward to
-the gradients of all six raw Gaussian parameter tensors.  Inputs are resident in HBM before the
-timed region.  With N ranks (one process per GPU, RCCL): every rank renders one full volume of
+samples per wall point, "cuda" preset, no occlusion), MSE against gt_times x a target volume,
+backward to the gradients of all six raw Gaussian parameter tensors, Adam update of the six
+parameter groups (nlosgr.train.TrainStep: the reference's learn_one_iter, main.py:198-214, over
+the whole volume).  Inputs are resident in HBM before the timed region.  With N ranks (one process per GPU, RCCL): every rank renders one full volume of
 its own capture (same scene, distinct target), gradients are summed with one all-reduce per
 step -> weak scaling, value = N volumes per step / max-over-ranks step time.
 
@@ -111,8 +112,9 @@ def main():
 
     from nlosgr import GaussianParams
     from nlosgr.model import features_flat
-    from nlosgr.render import render_backward, render_forward
-    from nlosgr.volume import Scene, make_config, volume_loss
+    from nlosgr.render import render_forward
+    from nlosgr.train import TrainStep
+    from nlosgr.volume import Scene, make_config
 
     ng, H, W, T, ns, fwd_only = CONFIGS[a.config]
     scene = Scene(H=H, W=W, T=T, ns=ns)
@@ -120,34 +122,26 @@ def main():
     geo = scene.geometry(dev, "cuda", "noocl")
     cfg = make_config(model, scene, "cuda", "noocl", cutoff=a.cutoff)
     g = torch.Generator().manual_seed(1 + rank)
-    target = (torch.rand(H * W, T, generator=g) * 1e-3 * 100).to(dev)   # gt_times=100 (configs/default.py:12)
-    feats = features_flat(model).detach().contiguous()
-    params = [model._mu.detach(), model._scaling.detach(), model._rotation.detach(), model._opacity.detach(), feats]
-    stream = torch.cuda.current_stream(dev)
+    target = (torch.rand(H * W, T, generator=g) * 1e-3).to(dev)   # measured volume, x gt_times=100 in the loss
     ev_fwd = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     ev_bwd = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     fwd_ms, bwd_ms = [], []
+    # one training iteration of the reference (main.py:198-214) over the whole volume, fused on the
+    # device: forward (records the ray cache) -> MSE vs gt_times * target + dL/dhist -> backward
+    # (walks the ray cache) -> [packed gradient all-reduce] -> Adam over the six parameter groups
+    train = TrainStep(model, geo, cfg, target, gt_times=100.0, nwall_total=H * W * world,
+                      events={"fwd": ev_fwd, "bwd": ev_bwd})
+    stream = torch.cuda.current_stream(dev)
 
     def step(timed):
-        if timed:
-            ev_fwd[0].record(stream)
-        # the forward records its in-support rays for the backward of the same step (ray cache)
-        hist, _, ws = render_forward(*params, geo, cfg, True, False, ray_cache=not fwd_only)
-        if timed:
-            ev_fwd[1].record(stream)
         if fwd_only:
+            params = [model._mu.detach(), model._scaling.detach(), model._rotation.detach(),
+                      model._opacity.detach(), features_flat(model).detach().contiguous()]
+            ev_fwd[0].record(stream)
+            hist, _ = render_forward(*params, geo, cfg, True, False)
+            ev_fwd[1].record(stream)
             return hist
-        # MSE (nlos_helpers.py:325) over the volume; dL/dhist computed in closed form
-        grad = (2.0 / hist.numel()) * (hist - target)
-        if timed:
-            ev_bwd[0].record(stream)
-        grads = render_backward(*params, geo, cfg, grad_hist=grad, workspace=ws, ray_cache=True)
-        if timed:
-            ev_bwd[1].record(stream)
-        if world > 1:
-            flat = torch.cat([t.reshape(-1) for t in grads])
-            dist.all_reduce(flat)
-        return grads
+        return train()
 
     for _ in range(a.warmup):
         step(False)
@@ -189,6 +183,8 @@ def main():
     traffic, traffic_src = pmc_traffic(a.config, kern)
     # secondary roofline: in-support evaluations (counting pass, untimed) x SURVEY FLOP convention
     from nlosgr.render import count_support
+    params = [model._mu.detach(), model._scaling.detach(), model._rotation.detach(), model._opacity.detach(),
+              features_flat(model).detach().contiguous()]
     pairs, rays, evals = count_support(*params, geo, cfg)
     flops = evals * FLOP_PER_EVAL[dom]
     valu = {"bound": "valu", "evaluations": evals, "pairs": pairs, "rays": rays,
@@ -203,7 +199,7 @@ def main():
         "dtype": "f32", "data": "synthetic (SURVEY §8d geometry, seeded random Gaussians and target)",
         "config": {"workload": f"{a.config}: {ng} Gaussians -> {H}x{W} wall x {T} bins, {ns}x{ns} angular "
                                f"samples, cuda preset, no occlusion, support cutoff {a.cutoff} sigma, "
-                               f"{'fwd' if fwd_only else 'fwd+MSE+bwd (6 param grads)'}",
+                               f"{'fwd' if fwd_only else 'fwd+MSE+bwd (6 param grads)+Adam'}",
                    "gaussians": ng, "wall": [H, W], "bins": T, "angular": ns, "cutoff": a.cutoff,
                    "parallelism": f"wall-replica x{world}, grad all-reduce" if world > 1 else "single GPU"},
         "phase_ms": {"fwd": fwd_avg, "bwd": bwd_avg},

@@ -16,6 +16,8 @@
  *   nlosgr_render_bwd   <- CUDARenderFunction.backward gaussian_model/cuda_autograd.py:110-191
  *                          (zeros in the reference; real gradients here) and torch autograd of path T
  *   nlosgr_rays_analytic <- _C.render_rays_analytic  src/volume_renderer_analytic.cu:178-241
+ *   nlosgr_mse / nlosgr_adam <- compute_loss nlos_helpers.py:323-327 + model.optimizer.step()
+ *                          main.py:203-213 (torch.optim.Adam groups, gaussian_model.py:223-242)
  *   nlosgr_bboxes       <- compute_gaussian_bboxes_kernel include/bbox_compute.cuh:76-120,
  *                          GaussianModel.get_bboxes gaussian_model/gaussian_model.py:140-178
  */
@@ -190,6 +192,37 @@ NLOSGR_API int nlosgr_rays_bwd(const nlosgr_gaussians* g, const nlosgr_rays* r, 
 NLOSGR_API int nlosgr_rays_analytic(const nlosgr_gaussians* g, const nlosgr_rays* r, const int32_t* filter,
                          float t_min, float t_max, float sigma_threshold, float* hist_out,
                          void* hip_stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Fused training step: the loss and the optimizer of the reference's
+ * learn_one_iter (main.py:198-254) on the device, with no host synchronisation.
+ * ------------------------------------------------------------------------------------- */
+#define NLOSGR_ADAM_MAX_GROUPS 8
+
+typedef struct {
+    float* param;             /* [n] updated in place */
+    const float* grad;        /* [n] */
+    float* exp_avg;           /* [n] first-moment state, updated in place (zeros before step 1) */
+    float* exp_avg_sq;        /* [n] second-moment state, updated in place */
+    long long n;
+    double lr;                /* this group's learning rate for this step */
+} nlosgr_adam_group;
+
+/* Volume MSE of compute_loss (nlos_helpers.py:323-327) over n elements, target scaled by gt_times:
+ * loss_out[2] = {mean((hist - gt*target)^2), loss / mean((gt*target)^2)} (device floats);
+ * grad_out [n] (may be NULL) = grad_scale * 2 (hist - gt*target) / n.  workspace: caller-owned,
+ * nlosgr_mse_workspace_bytes() bytes.  Deterministic (fixed-order reduction, no atomics). */
+NLOSGR_API size_t nlosgr_mse_workspace_bytes(void);
+NLOSGR_API int nlosgr_mse(const float* hist, const float* target, float gt_times, long long n,
+               float grad_scale, float* grad_out, void* workspace, float* loss_out, void* hip_stream);
+
+/* One torch.optim.Adam step (no weight decay, no amsgrad) over 1..NLOSGR_ADAM_MAX_GROUPS parameter
+ * groups; `step` >= 1 is the step count including this update (bias correction).  The scalars are
+ * doubles so 1 - beta, the bias corrections and lr / (1 - beta1^t) are formed as torch forms them
+ * (Python floats) before the fp32 update.  The reference
+ * uses betas (0.9, 0.999), eps 1e-15 and six groups (gaussian_model.py:223-242). */
+NLOSGR_API int nlosgr_adam(const nlosgr_adam_group* groups, int32_t ngroups, long long step, double beta1,
+                double beta2, double eps, void* hip_stream);
 
 NLOSGR_API const char* nlosgr_last_error(void);
 NLOSGR_API int nlosgr_abi_version(void);

@@ -54,6 +54,22 @@ using namespace nlosgr::detail;
 #ifndef NLOSGR_BWD_PF
 #define NLOSGR_BWD_PF 0        // backward: prefetch the next wall point's gradient row / tables
 #endif
+// kRecurrence: along a segment the log2 value is quadratic in the bin offset t, e(t) = ga t^2 + al,
+// so value(t+1) = value(t) * 2^(ga (2t+1)) and that ratio itself scales by 2^(2 ga) per bin.  The
+// culled drains (forward and backward, no-occlusion) re-seed value and ratio with exact exp2 once
+// per kSteps-bin round and multiply in between: relative error <= kSteps ulp.  Inside the support
+// |ga| t^2 <= m_c^2 log2(e) / 2, which bounds |ga (2t+1)| by m_c^2 log2(e) (<= 47 at m_c = 5.7),
+// so the ratio never overflows; past the segment end both factors only shrink (no inf * 0).
+// Dense mode (unbounded t) keeps the per-bin exp2.
+#ifndef NLOSGR_FREC
+#define NLOSGR_FREC 1          // forward no-occlusion drain: exp2 recurrence
+#endif
+#ifndef NLOSGR_FQUAD
+#define NLOSGR_FQUAD 1         // forward culled no-occlusion drain: float4 read-add-write per 4 bins
+#endif
+#ifndef NLOSGR_BREC
+#define NLOSGR_BREC 1          // backward no-occlusion drain: exp2 recurrence + per-round moment sums
+#endif
 
 namespace {
 
@@ -422,6 +438,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_F
     const float rscale = k.opt.ray_scale;
     const int flags = k.opt.flags;
     const int pad = nr + kSteps + lane;       // this lane's private pad bins (non-winners)
+    const int padq = al4(nr + kSteps);        // quad drain: one pad quad row shared by non-winners (they add 0)
     unsigned npair = 0, nseg = 0;
     unsigned long long nsamp = 0;
 
@@ -526,17 +543,67 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_F
                 continue;
             }
             if (!anymore && qcount == 0 && have) break;   // next Gaussians; segments carry over
-            // claim distinct start bins
-            if (act) owner[d.pos] = (unsigned char)lane;
+            // claim distinct start bins (quad drain: distinct start quads)
+            constexpr bool QUAD = NLOSGR_FQUAD && NLOSGR_FREC && MODE == NLOSGR_MODE_NOOCL && !RAYS && !DENSE;
+            const int key = QUAD ? (d.pos >> 2) : d.pos;
+            if (act) owner[key] = (unsigned char)lane;
             wave_sync();
-            const bool win = act && owner[d.pos] == (unsigned char)lane;
+            const bool win = act && owner[key] == (unsigned char)lane;
             wave_sync();
             const int remw = win ? d.rem : 0;
-            float* hb = hist + (win ? d.pos : pad);
+            float* hb = hist + (win ? (QUAD ? (d.pos & ~3) : d.pos) : (QUAD ? padq : pad));
             float t = d.t;
             float logT = d.logT;
             float xlo = d.xlo, elo = d.elo;
-            if (NLOSGR_FPACKED && MODE == NLOSGR_MODE_NOOCL && !RAYS) {
+            if (QUAD) {
+                // 16 bins from the quad holding pos: one ds_read_b128 + ds_write_b128 per 4 bins (the
+                // b32 read-add-write is bank-conflict bound).  Slots before pos (first round of a
+                // segment only) add 0 and do not advance the recurrence, which starts at pos.
+                const int o = d.pos & 3;
+                float cur = fast_exp2(fmaf(d.ga, t * t, d.al));
+                float q = fast_exp2(d.ga * fmaf(2.f, t, 1.f));
+                const float cc = fast_exp2(2.f * d.ga);
+                float4* hb4 = reinterpret_cast<float4*>(hb);
+#pragma unroll
+                for (int k4 = 0; k4 < kSteps / 4; ++k4) {
+                    float v[4];
+#pragma unroll
+                    for (int jj = 0; jj < 4; ++jj) {
+                        const int j = 4 * k4 + jj;
+                        if (k4 == 0) {
+                            const bool st = jj >= o;
+                            v[jj] = (st && j - o < remw) ? cur : 0.f;
+                            cur = st ? cur * q : cur;
+                            q = st ? q * cc : q;
+                        } else {
+                            v[jj] = j - o < remw ? cur : 0.f;
+                            cur *= q;
+                            q *= cc;
+                        }
+                    }
+                    float4 x = hb4[k4];
+                    x.x += v[0]; x.y += v[1]; x.z += v[2]; x.w += v[3];
+                    hb4[k4] = x;
+                    compiler_fence();
+                }
+                t += (float)(kSteps - o);
+            } else if (NLOSGR_FREC && MODE == NLOSGR_MODE_NOOCL && !RAYS && !DENSE) {
+                // value(t+1) = value(t) q(t), q(t+1) = q(t) 2^(2 ga): two multiplies per bin instead of
+                // mul + fma + exp2; seeded with exact exp2 every round (see kRecurrence)
+                float cur = fast_exp2(fmaf(d.ga, t * t, d.al));
+                float q = fast_exp2(d.ga * fmaf(2.f, t, 1.f));
+                const float cc = fast_exp2(2.f * d.ga);
+#pragma unroll
+                for (int m = 0; m < kSteps; ++m) {
+                    const float v = m < remw ? cur : 0.f;
+                    cur *= q;
+                    q *= cc;
+                    const float x = hb[m];
+                    hb[m] = x + v;
+                    compiler_fence();
+                }
+                t += (float)kSteps;
+            } else if (NLOSGR_FPACKED && MODE == NLOSGR_MODE_NOOCL && !RAYS) {
                 // two bins per v_pk_mul/v_pk_fma/v_pk_add; the LDS read-add-write stays in bin order
                 f32x2 tv = {t, t + 1.f};
                 const f32x2 gav = {d.ga, d.ga}, alv = {d.al, d.al};
@@ -594,12 +661,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_F
                 compiler_fence();
             }
             if (win) {
+                const int adv = QUAD ? kSteps - (d.pos & 3) : kSteps;
                 d.t = t;
                 d.logT = logT;
                 d.xlo = xlo;
                 d.elo = elo;
-                d.pos += kSteps;
-                d.rem -= kSteps;
+                d.pos += adv;
+                d.rem -= adv;
                 act = d.rem > 0;
             }
         }
@@ -963,6 +1031,27 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_B
                     b.S0 = S0.x + S0.y; b.S1 = S1.x + S1.y; b.S2 = S2.x + S2.y;
 #else
                     float S0 = b.S0, S1 = b.S1, S2 = b.S2;
+                    if (NLOSGR_BREC && !DENSE) {
+                        // exp2 recurrence (kRecurrence) and moments about the round's first bin:
+                        // U_n = sum_m hp m^n, then S_n += sum_m hp (kap + m)^n
+                        float pdf = fast_exp2(fmaf(b.c2, kap * kap, b.c0));
+                        float q = fast_exp2(b.c2 * fmaf(2.f, kap, 1.f));
+                        const float cc = fast_exp2(2.f * b.c2);
+                        float U0 = 0.f, U1 = 0.f, U2 = 0.f;
+#pragma unroll
+                        for (int m = 0; m < kBSteps; ++m) {
+                            const float hp = Hs[m] * pdf;
+                            U0 += hp;
+                            U1 = fmaf(hp, (float)m, U1);
+                            U2 = fmaf(hp, (float)(m * m), U2);
+                            pdf *= q;
+                            q *= cc;
+                        }
+                        S0 += U0;
+                        S1 += fmaf(kap, U0, U1);
+                        S2 += fmaf(kap, fmaf(kap, U0, 2.f * U1), U2);
+                        kap += (float)kBSteps;
+                    } else
 #pragma unroll
                     for (int m = 0; m < kBSteps; ++m) {
                         const float hp = Hs[m] * fast_exp2(fmaf(b.c2, kap * kap, b.c0));

@@ -47,13 +47,20 @@ class Rays(ctypes.Structure):
                 ("t", _P), ("cam", _P)]
 
 
+class AdamGroup(ctypes.Structure):
+    _fields_ = [("param", _P), ("grad", _P), ("exp_avg", _P), ("exp_avg_sq", _P), ("n", ctypes.c_longlong),
+                ("lr", ctypes.c_double)]
+
+
+ADAM_MAX_GROUPS = 8  # NLOSGR_ADAM_MAX_GROUPS
 MAX_PER_RAY = 256   # NLOSGR_MAX_PER_RAY
 ABI_VERSION = 2     # NLOSGR_ABI_VERSION
 
 # every symbol include/nlosgr.h declares (tests check the exports against this list)
 EXPORTS = ["nlosgr_workspace_bytes", "nlosgr_render_fwd", "nlosgr_render_bwd", "nlosgr_count_support",
            "nlosgr_bboxes", "nlosgr_rays_workspace_bytes", "nlosgr_filter_rays", "nlosgr_rays_fwd",
-           "nlosgr_rays_bwd", "nlosgr_rays_analytic", "nlosgr_last_error", "nlosgr_abi_version"]
+           "nlosgr_rays_bwd", "nlosgr_rays_analytic", "nlosgr_mse_workspace_bytes", "nlosgr_mse", "nlosgr_adam",
+           "nlosgr_last_error", "nlosgr_abi_version"]
 
 _lib = None
 _load_error = None
@@ -89,6 +96,13 @@ def load():
     lib.nlosgr_rays_bwd.restype = ctypes.c_int
     lib.nlosgr_rays_analytic.argtypes = [PG, PR, _P, ctypes.c_float, ctypes.c_float, ctypes.c_float, _P, _P]
     lib.nlosgr_rays_analytic.restype = ctypes.c_int
+    lib.nlosgr_mse_workspace_bytes.argtypes = []
+    lib.nlosgr_mse_workspace_bytes.restype = ctypes.c_size_t
+    lib.nlosgr_mse.argtypes = [_P, _P, ctypes.c_float, ctypes.c_longlong, ctypes.c_float, _P, _P, _P, _P]
+    lib.nlosgr_mse.restype = ctypes.c_int
+    lib.nlosgr_adam.argtypes = [ctypes.POINTER(AdamGroup), ctypes.c_int32, ctypes.c_longlong, ctypes.c_double,
+                                ctypes.c_double, ctypes.c_double, _P]
+    lib.nlosgr_adam.restype = ctypes.c_int
     lib.nlosgr_bboxes.argtypes = [PG, ctypes.c_float, _P, _P]
     lib.nlosgr_bboxes.restype = ctypes.c_int
     lib.nlosgr_last_error.argtypes = []

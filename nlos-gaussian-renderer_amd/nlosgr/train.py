@@ -1,0 +1,196 @@
+"""Fused on-device training step over the whole transient volume.
+
+The reference's training iteration (main.py:198-254 learn_one_iter) is, per wall point:
+update_learning_rate -> zero_grad -> compute_loss (render + MSE vs gt_times * data,
+nlos_helpers.py:280-346) -> backward -> optimizer.step (torch.optim.Adam over six parameter
+groups, gaussian_model.py:223-242) -> oneupSHdegree (main.py:240-241).  TrainStep runs the same
+iteration for a whole volume (or this rank's band of it) with every piece on the device and no
+host synchronisation inside the step:
+
+    render_forward (HIP, records the ray cache)  ->  nlosgr_mse (loss, equal_loss, dL/dhist)
+    ->  render_backward (HIP, walks the ray cache)  ->  [one packed all-reduce when sharded]
+    ->  nlosgr_adam (all six groups in one launch; position lr from get_expon_lr_func)
+
+The returned loss is a device tensor; reading it is the caller's choice (and its only sync).
+"""
+import math
+from dataclasses import dataclass, replace
+
+import torch
+import torch.distributed as dist
+
+from . import _lib
+from .model import features_flat
+from .render import render_backward, render_forward, use_ray_cache
+
+GROUPS = ("mu", "f_dc", "f_rest", "opacity", "scaling", "rotation")   # gaussian_model.py:229-236
+
+
+def expon_lr(step, lr_init, lr_final, lr_delay_steps=0, lr_delay_mult=1.0, max_steps=1000000):
+    """get_expon_lr_func(...)(step) (gaussian_utils.py:223-256): log-linear decay from lr_init to
+    lr_final over max_steps, optionally eased in over lr_delay_steps."""
+    if step < 0 or (lr_init == 0.0 and lr_final == 0.0):
+        return 0.0
+    if lr_delay_steps > 0:
+        delay_rate = lr_delay_mult + (1 - lr_delay_mult) * math.sin(0.5 * math.pi * min(max(step / lr_delay_steps,
+                                                                                           0.0), 1.0))
+    else:
+        delay_rate = 1.0
+    t = min(max(step / max_steps, 0.0), 1.0)
+    return delay_rate * math.exp(math.log(lr_init) * (1 - t) + math.log(lr_final) * t)
+
+
+@dataclass
+class OptimizationParams:
+    """The optimiser fields of configs/default.py:59-69 (OptimizationParams) the step uses."""
+    position_lr_init: float = 0.00016
+    position_lr_final: float = 0.0000016
+    position_lr_delay_mult: float = 0.01
+    position_lr_max_steps: int = 50_000
+    feature_lr: float = 0.0025
+    opacity_lr: float = 0.025
+    scaling_lr: float = 0.005
+    rotation_lr: float = 0.001
+    regularization: bool = False     # configs/default.py:88-90, applied in learn_one_iter (main.py:204-208)
+    scale_reg: float = 0.01
+    opacity_reg: float = 0.01
+
+
+def mse(hist, target, gt_times=1.0, grad_scale=1.0, want_grad=True):
+    """(loss2, grad): loss2 = device [2] = (MSE, equal_loss) of compute_loss
+    (nlos_helpers.py:323-327) against gt_times * target; grad = grad_scale * dMSE/dhist."""
+    lib = _lib.load()
+    dev = hist.device
+    h = hist.detach().contiguous()
+    t = target.detach().contiguous()
+    if h.shape != t.shape or h.dtype != torch.float32 or t.dtype != torch.float32:
+        raise ValueError("nlosgr: hist and target must be float32 tensors of one shape")
+    ws = torch.empty(lib.nlosgr_mse_workspace_bytes() // 4, dtype=torch.float32, device=dev)
+    out = torch.empty(2, dtype=torch.float32, device=dev)
+    grad = torch.empty_like(h) if want_grad else None
+    _lib.check(lib.nlosgr_mse(_lib.ptr(h), _lib.ptr(t), float(gt_times), h.numel(), float(grad_scale),
+                              _lib.ptr(grad), _lib.ptr(ws), _lib.ptr(out), _lib.stream_handle(dev)))
+    return out, grad
+
+
+class Adam:
+    """torch.optim.Adam (no weight decay / amsgrad) on the device for a fixed list of contiguous
+    fp32 tensors, one launch per step (nlosgr_adam)."""
+
+    def __init__(self, params, betas=(0.9, 0.999), eps=1e-15):
+        if not 1 <= len(params) <= _lib.ADAM_MAX_GROUPS:
+            raise ValueError("nlosgr: 1..8 parameter groups")
+        for p in params:
+            if p.dtype != torch.float32 or not p.is_contiguous() or not p.is_cuda:
+                raise ValueError("nlosgr: Adam parameters must be contiguous float32 GPU tensors")
+        self.params = list(params)
+        self.exp_avg = [torch.zeros_like(p) for p in params]
+        self.exp_avg_sq = [torch.zeros_like(p) for p in params]
+        self.betas, self.eps, self.step_count = betas, eps, 0
+
+    def step(self, grads, lrs):
+        lib = _lib.load()
+        self.step_count += 1
+        gs = []
+        arr = (_lib.AdamGroup * len(self.params))()
+        for i, (p, g, lr) in enumerate(zip(self.params, grads, lrs)):
+            g = g.detach().reshape(p.shape).contiguous()
+            gs.append(g)   # keep alive until the launch is enqueued
+            arr[i] = _lib.AdamGroup(_lib.ptr(p), _lib.ptr(g), _lib.ptr(self.exp_avg[i]),
+                                    _lib.ptr(self.exp_avg_sq[i]), p.numel(), float(lr))
+        _lib.check(lib.nlosgr_adam(arr, len(self.params), self.step_count, float(self.betas[0]),
+                                   float(self.betas[1]), float(self.eps), _lib.stream_handle(self.params[0].device)))
+
+
+class TrainStep:
+    """One fused training iteration per call (see module docstring).
+
+    model   : GaussianModel-like (raw tensors _mu, _scaling, _rotation, _opacity, _features_dc,
+              _features_rest and active_sh_degree); updated in place.
+    geo     : nlosgr Geometry of the wall points this process renders (the whole wall, or this
+              rank's band from nlosgr.distributed.wall_band).
+    target  : [P, T] measured histograms of those wall points (before gt_times).
+    nwall_total : wall points of the whole volume (the MSE is normalised over the whole volume and
+              the band gradients / losses are summed over ranks).
+    """
+
+    def __init__(self, model, geo, cfg, target, gt_times=1.0, opt=None, spatial_lr_scale=1.0, nwall_total=None,
+                 group=None, sh_schedule=False, events=None):
+        self.model, self.geo, self.cfg = model, geo, cfg
+        self.target = target.detach().float().contiguous()
+        self.gt_times = float(gt_times)
+        self.opt = opt or OptimizationParams()
+        self.spatial_lr_scale = float(spatial_lr_scale)
+        self.group = group
+        self.world = dist.get_world_size(group) if (dist.is_available() and dist.is_initialized()) else 1
+        self.n_local = geo.nwall * geo.nr
+        self.n_total = (nwall_total if nwall_total is not None else geo.nwall) * geo.nr
+        self.sh_schedule = sh_schedule
+        self.events = events      # optional {"fwd": (start, end), "bwd": (start, end)} HIP events (bench timing)
+        self.iteration = 0
+        ng = model._mu.shape[0]
+        self._tensors = [model._mu.data, model._features_dc.data.view(ng, -1), model._features_rest.data.view(ng, -1),
+                         model._opacity.data.view(ng), model._scaling.data, model._rotation.data]
+        self.adam = Adam(self._tensors, eps=1e-15)
+
+    def learning_rates(self, iteration):
+        o = self.opt
+        mu_lr = expon_lr(iteration, o.position_lr_init * self.spatial_lr_scale,
+                         o.position_lr_final * self.spatial_lr_scale, lr_delay_mult=o.position_lr_delay_mult,
+                         max_steps=o.position_lr_max_steps)     # update_learning_rate, gaussian_model.py:244-249
+        return [mu_lr, o.feature_lr, o.feature_lr / 20.0, o.opacity_lr, o.scaling_lr, o.rotation_lr]
+
+    def __call__(self, iteration=None):
+        it = self.iteration if iteration is None else iteration
+        m = self.model
+        ng = m._mu.shape[0]
+        cfg = replace(self.cfg, sh_degree=int(m.active_sh_degree))
+        feats = features_flat(m).detach().contiguous()
+        args = (m._mu.detach(), m._scaling.detach(), m._rotation.detach(), m._opacity.detach(), feats, self.geo)
+        cache = use_ray_cache(cfg, self.geo, ng)
+        ev = self.events
+        stream = torch.cuda.current_stream(m._mu.device) if ev else None
+        if ev:
+            ev["fwd"][0].record(stream)
+        out = render_forward(*args, cfg, True, False, ray_cache=cache)
+        if ev:
+            ev["fwd"][1].record(stream)
+        hist, ws = out[0], (out[2] if cache else None)
+        loss2, grad = mse(hist, self.target, self.gt_times, grad_scale=self.n_local / self.n_total)
+        if ev:
+            ev["bwd"][0].record(stream)
+        d_mu, d_s, d_q, d_o, d_f = render_backward(*args, cfg, grad_hist=grad, workspace=ws, ray_cache=cache)
+        if ev:
+            ev["bwd"][1].record(stream)
+        del ws
+        grads = [d_mu, d_f[:, :1], d_f[:, 1:], d_o, d_s, d_q]
+        if self.world > 1:
+            flat = torch.cat([g.reshape(-1) for g in grads])
+            dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group)
+            off, split = 0, []
+            for g in grads:
+                split.append(flat[off:off + g.numel()].view(g.shape))
+                off += g.numel()
+            grads = split
+            # global loss and equal_loss from the band means (device ops; no host sync)
+            frac = self.n_local / self.n_total
+            se = loss2[0] * frac
+            st = loss2[0] / loss2[1] * frac
+            both = torch.stack([se, st])
+            dist.all_reduce(both, op=dist.ReduceOp.SUM, group=self.group)
+            loss2 = torch.stack([both[0], both[0] / both[1]])
+        if self.opt.regularization:
+            # + opacity_reg mean|sigmoid(o)| + scale_reg mean|exp(s)| (main.py:204-208); replicated
+            # terms, so added after the all-reduce.  equal_loss stays the render term's (as there).
+            o = m._opacity.detach().reshape(-1)
+            so = torch.sigmoid(o)
+            es = torch.exp(m._scaling.detach())
+            grads[3] = grads[3] + (self.opt.opacity_reg / o.numel()) * so * (1.0 - so)
+            grads[4] = grads[4] + (self.opt.scale_reg / es.numel()) * es
+            reg = self.opt.opacity_reg * so.mean() + self.opt.scale_reg * es.mean()
+            loss2 = torch.stack([loss2[0] + reg, loss2[1]])
+        self.adam.step(grads, self.learning_rates(it))
+        self.iteration = it + 1
+        if self.sh_schedule and self.iteration % 1000:   # main.py:240-241 (fires when NOT a multiple)
+            m.oneupSHdegree()
+        return loss2

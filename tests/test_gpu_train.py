@@ -1,0 +1,152 @@
+"""GPU parity of the fused training step through the C ABI.
+
+  nlosgr_mse   vs the fp64 expression of compute_loss (nlos_helpers.py:323-327):
+               loss / equal_loss rel <= 1e-5, grad vs the torch fp32 expression rel <= 1e-6
+  nlosgr_adam  vs torch.optim.Adam(eps=1e-15) with the reference's six groups
+               (gaussian_model.py:223-242) over 5 steps: params / moments rel <= 1e-6 of max
+  TrainStep    vs the same iteration composed from torch pieces (RenderFn autograd + torch MSE
+               [+ the optional regularisers] + torch.optim.Adam, main.py:198-214) on identical
+               inputs over 3 iterations: params rel <= 1e-5 of max
+"""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-30)).item()
+
+
+@pytest.mark.parametrize("n", [1, 1000, 257 * 1031, 3 * 1024 * 1024 + 5])
+def test_mse_matches_torch(n):
+    from nlosgr.train import mse
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device="cpu").manual_seed(n)
+    hist = torch.rand(n, generator=g).to(dev)
+    target = (torch.rand(n, generator=g) * 1e-2).to(dev)
+    gt_times = 100.0
+    loss2, grad = mse(hist, target, gt_times, grad_scale=0.5)
+    t = target.double() * gt_times
+    d = hist.double() - t
+    ref_loss = (d * d).mean()
+    ref_eq = ref_loss / (t * t).mean()
+    assert abs(loss2[0].item() - ref_loss.item()) <= 1e-5 * ref_loss.item()
+    assert abs(loss2[1].item() - ref_eq.item()) <= 1e-5 * ref_eq.item()
+    # gradient of 0.5 * mean((hist - gt target)^2) w.r.t. hist
+    ref_grad = (0.5 * 2.0 / n) * (hist - target * gt_times)
+    assert _rel(grad, ref_grad) <= 1e-6
+
+
+def test_mse_empty_and_errors():
+    from nlosgr import _lib
+    from nlosgr.train import mse
+    dev = torch.device("cuda:0")
+    e = torch.empty(0, device=dev)
+    loss2, grad = mse(e, e)
+    assert loss2.tolist() == [0.0, 0.0] and grad.numel() == 0
+    with pytest.raises(ValueError):
+        mse(torch.zeros(4, device=dev), torch.zeros(5, device=dev))
+    lib = _lib.load()
+    assert lib.nlosgr_mse(None, None, 1.0, -1, 1.0, None, None, None, None) != 0
+    assert b"n must be" in lib.nlosgr_last_error()
+
+
+def _groups(dev, ng=5000, seed=0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    shapes = [(ng, 3), (ng, 1), (ng, 15), (ng,), (ng, 3), (ng, 4)]
+    return [torch.randn(*s, generator=g).to(dev) for s in shapes]
+
+
+def test_adam_matches_torch_optim():
+    from nlosgr.train import Adam
+    dev = torch.device("cuda:0")
+    ours = [t.clone() for t in _groups(dev)]
+    ref = [torch.nn.Parameter(t.clone()) for t in ours]
+    lrs = [1.6e-4, 2.5e-3, 2.5e-3 / 20, 2.5e-2, 5e-3, 1e-3]
+    opt = torch.optim.Adam([{"params": [p], "lr": lr} for p, lr in zip(ref, lrs)], lr=0.0, eps=1e-15,
+                           foreach=False)
+    mine = Adam(ours, eps=1e-15)
+    g = torch.Generator(device="cpu").manual_seed(7)
+    for step in range(5):
+        grads = [(torch.randn(p.shape, generator=g) * 10.0 ** (step - 3)).to(dev) for p in ours]
+        step_lrs = [lr * (0.9 ** step) for lr in lrs]
+        for p, gr, lr, grp in zip(ref, grads, step_lrs, opt.param_groups):
+            p.grad = gr.clone()
+            grp["lr"] = lr
+        opt.step()
+        mine.step(grads, step_lrs)
+    torch.cuda.synchronize()
+    for a, b in zip(ours, ref):
+        assert _rel(a, b) <= 1e-6
+    for i, b in enumerate(ref):
+        st = opt.state[b]
+        assert _rel(mine.exp_avg[i], st["exp_avg"]) <= 1e-6
+        assert _rel(mine.exp_avg_sq[i], st["exp_avg_sq"]) <= 1e-6
+
+
+def test_adam_rejects_bad_args():
+    from nlosgr import _lib
+    from nlosgr.train import Adam
+    dev = torch.device("cuda:0")
+    with pytest.raises(ValueError):
+        Adam([torch.zeros(3, device=dev, dtype=torch.float64)])
+    with pytest.raises(ValueError):
+        Adam([torch.zeros(3, device=dev)] * 9)
+    lib = _lib.load()
+    arr = (_lib.AdamGroup * 1)()
+    assert lib.nlosgr_adam(arr, 1, 0, 0.9, 0.999, 1e-15, None) != 0
+    assert b"step" in lib.nlosgr_last_error()
+
+
+def _scene_model(dev, ng=400, H=6, W=5, T=48, seed=3):
+    from nlosgr import GaussianParams
+    from nlosgr.volume import Scene, make_config
+    scene = Scene(H=H, W=W, T=T, ns=8)
+    model = GaussianParams.synthetic(ng, 3, preset="cuda", device=dev, seed=seed)
+    geo = scene.geometry(dev, "cuda", "noocl")
+    cfg = make_config(model, scene, "cuda", "noocl", cutoff=3.0)
+    g = torch.Generator().manual_seed(seed + 1)
+    target = (torch.rand(H * W, T, generator=g) * 1e-3).to(dev)
+    return scene, model, geo, cfg, target
+
+
+@pytest.mark.parametrize("regularization", [False, True])
+def test_train_step_matches_torch_composition(regularization):
+    """Three fused TrainStep iterations == render autograd + torch MSE + torch.optim.Adam."""
+    from nlosgr import GaussianParams
+    from nlosgr.train import OptimizationParams, TrainStep
+    from nlosgr.volume import render_volume
+    dev = torch.device("cuda:0")
+    scene, model, geo, cfg, target = _scene_model(dev)
+    twin = GaussianParams(*(p.detach().clone() for p in model.parameters()), model.active_sh_degree)
+    gt_times = 100.0
+    opt = OptimizationParams(regularization=regularization)
+    step = TrainStep(model, geo, cfg, target, gt_times=gt_times, opt=opt, spatial_lr_scale=2.0)
+    names = ["mu", "scaling", "rotation", "opacity", "f_dc", "f_rest"]     # GaussianParams.parameters() order
+    by_name = dict(zip(names, twin.parameters()))
+    lr0 = {"mu": opt.position_lr_init * 2.0, "f_dc": opt.feature_lr, "f_rest": opt.feature_lr / 20.0,
+           "opacity": opt.opacity_lr, "scaling": opt.scaling_lr, "rotation": opt.rotation_lr}
+    order = ["mu", "f_dc", "f_rest", "opacity", "scaling", "rotation"]       # gaussian_model.py:229-236
+    torch_opt = torch.optim.Adam([{"params": [by_name[n]], "lr": lr0[n], "name": n} for n in order], lr=0.0,
+                                 eps=1e-15, foreach=False)
+    for it in range(3):
+        loss2 = step(it)
+        torch_opt.param_groups[0]["lr"] = step.learning_rates(it)[0]
+        torch_opt.zero_grad()
+        hist = render_volume(twin, geo, cfg)
+        t = target * gt_times
+        loss = ((hist - t) ** 2).mean()
+        if regularization:
+            loss = loss + opt.opacity_reg * torch.abs(torch.sigmoid(twin._opacity)).mean()
+            loss = loss + opt.scale_reg * torch.abs(torch.exp(twin._scaling)).mean()
+        loss.backward()
+        torch_opt.step()
+        assert abs(loss2[0].item() - loss.item()) <= 1e-5 * loss.item()
+    torch.cuda.synchronize()
+    for n, a, b in zip(names, model.parameters(), twin.parameters()):
+        assert _rel(a, b) <= 1e-5, n

@@ -1,0 +1,26 @@
+"""Host logic of the fused training step that needs no GPU: the position learning-rate schedule
+(get_expon_lr_func, gaussian_utils.py:223-256) and the optimiser defaults (configs/default.py:59-90)."""
+import math
+
+import pytest
+
+
+def test_expon_lr_schedule():
+    from nlosgr.train import expon_lr
+    assert expon_lr(0, 1e-3, 1e-5, max_steps=100) == pytest.approx(1e-3)
+    assert expon_lr(100, 1e-3, 1e-5, max_steps=100) == pytest.approx(1e-5)
+    assert expon_lr(250, 1e-3, 1e-5, max_steps=100) == pytest.approx(1e-5)      # clipped past max_steps
+    assert expon_lr(50, 1e-3, 1e-5, max_steps=100) == pytest.approx(1e-4)
+    assert expon_lr(-1, 1e-3, 1e-5) == 0.0
+    assert expon_lr(3, 0.0, 0.0) == 0.0
+    d = expon_lr(5, 1e-3, 1e-3, lr_delay_steps=10, lr_delay_mult=0.01, max_steps=100)
+    assert d == pytest.approx(1e-3 * (0.01 + 0.99 * math.sin(0.25 * math.pi)))
+
+
+def test_optimization_defaults_match_reference_config():
+    from nlosgr.train import OptimizationParams
+    o = OptimizationParams()
+    assert (o.position_lr_init, o.position_lr_final, o.position_lr_delay_mult, o.position_lr_max_steps) == \
+        (0.00016, 0.0000016, 0.01, 50_000)
+    assert (o.feature_lr, o.opacity_lr, o.scaling_lr, o.rotation_lr) == (0.0025, 0.025, 0.005, 0.001)
+    assert (o.regularization, o.scale_reg, o.opacity_reg) == (False, 0.01, 0.01)
