@@ -64,6 +64,9 @@ using namespace nlosgr::detail;
 #ifndef NLOSGR_FREC
 #define NLOSGR_FREC 1          // forward no-occlusion drain: exp2 recurrence
 #endif
+#ifndef NLOSGR_DIAG
+#define NLOSGR_DIAG 0          // utilisation counters under opt.flags 8 / 16 (scripts/drain_diag.py builds)
+#endif
 #ifndef NLOSGR_FQUAD
 #define NLOSGR_FQUAD 1         // forward culled no-occlusion drain: float4 read-add-write per 4 bins
 #endif
@@ -88,6 +91,9 @@ struct KArgs {
     int nsplit;
     unsigned long long* counts;  // optional [3]: pairs, segments, samples (nlosgr_count_support)
     ulonglong2* cmask;           // ray cache [P][ng]: passing rays of the pair's box (bit = box cell)
+    float* drho;                 // backward: dL/drho per pair [P][ng] (0 outside the support) -> sh_kernel
+    float* shpart;               // sh_kernel partials [nsh][ng][kShPart]
+    int nsh;                     // sh_kernel wall-point splits
     unsigned* cbox;              // ray cache [P][ng]: i0 | j0 << 12 | width << 24, 0 = not cached
 };
 
@@ -491,7 +497,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_F
                 lwc = more ? flog2(P.w * cdt) : 0.f;
             }
             if (flags & 2) more = false;      // diagnostics: pair setup only
-            npair += __builtin_popcountll(__builtin_amdgcn_ballot_w64(more));
+            if (!(NLOSGR_DIAG && (flags & 8))) npair += __builtin_popcountll(__builtin_amdgcn_ballot_w64(more));
+            if (NLOSGR_DIAG && (flags & 16))   // diagnostics: candidate cells instead of samples
+                nsamp += more ? (unsigned)((P.i1 - P.i0 + 1) * (P.j1 - P.j0 + 1)) : 0u;
             ci = P.i0; cj = P.j0;
 #if NLOSGR_FWD_PF
             if (base + kBlock < k.g.ng) {   // prefetch the next chunk
@@ -529,10 +537,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_F
                 if (take && !(flags & 1)) {
                     got = drain_setup<MODE, DENSE, RAYS>(A, u0, lws, scs, lwcs, tth[i], tph[j], i, j, np_, nr, mc2,
                                                          r0, dr, inv_dr, f0log2, d);
-                    if (got) nsamp += (unsigned)d.rem;
+                    if (got && !(NLOSGR_DIAG && (flags & 24))) nsamp += (unsigned)d.rem;
                     act = got && !(flags & 4);    // diagnostics: segment records only
                 }
-                nseg += __popcll(__builtin_amdgcn_ballot_w64(got));
+                if (!(NLOSGR_DIAG && (flags & 8))) nseg += __popcll(__builtin_amdgcn_ballot_w64(got));
                 const int ntake = min(nidle, qcount);
                 qhead = (qhead + ntake) & (kRQ - 1);
                 qcount -= ntake;
@@ -551,6 +559,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_F
             const bool win = act && owner[key] == (unsigned char)lane;
             wave_sync();
             const int remw = win ? d.rem : 0;
+            if (NLOSGR_DIAG && (flags & 8)) {   // diagnostics (count_support): rounds, active / winning lanes
+                npair += 1;
+                nseg += __popcll(__builtin_amdgcn_ballot_w64(act));
+                nsamp += __popcll(__builtin_amdgcn_ballot_w64(win));
+            }
             float* hb = hist + (win ? (QUAD ? (d.pos & ~3) : d.pos) : (QUAD ? padq : pad));
             float t = d.t;
             float logT = d.logT;
@@ -684,7 +697,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_F
     }
     if (k.counts) {
         unsigned long long ns = nsamp;
-        for (int o = 32; o > 0; o >>= 1) ns += __shfl_xor(ns, o);
+        if (!(NLOSGR_DIAG && (flags & 8)))
+            for (int o = 32; o > 0; o >>= 1) ns += __shfl_xor(ns, o);
         if (lane == 0) {
             atomicAdd(k.counts, (unsigned long long)npair);
             atomicAdd(k.counts + 1, (unsigned long long)nseg);
@@ -712,6 +726,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_F
 // claimant's result with ds_bpermute and folds it into the Gaussian's register accumulators.
 // Losers keep their result and retry next round.  No LDS float atomics, no pair/row tables.
 constexpr int kBSteps = 16;
+constexpr int kBwdSlots = 13;   // per-Gaussian backward partial: dA[9], dMu[3], dsigma (stride 32 in HBM)
+constexpr int kShPart = 20;     // sh_kernel partial: dF[16], dMu[3], pad
 
 struct BwdLayout {
     int wave_base, wave_stride, grow, tth, tph, rayq, owner, pdat, red, total;
@@ -726,7 +742,7 @@ struct BwdLayout {
         wave_stride = al4(pdat + 64 * 16);
         red = wave_base;                     // final reduction reuses the wave regions
         total = wave_base + kWaves * wave_stride;
-        const int need_red = wave_base + kWaves * 64 * 29;
+        const int need_red = wave_base + kWaves * 64 * kBwdSlots;
         if (need_red > total) total = need_red;
     }
 };
@@ -875,11 +891,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_B
     const float f0log2 = log2f(1.0f + 1e-7f);
     const float rscale = k.opt.ray_scale;
 
-    float dA[9], dMu[3], dSig = 0.f, dF[kMaxK];
+    float dA[9], dMu[3], dSig = 0.f;
+    unsigned long long dg[5] = {0ull, 0ull, 0ull, 0ull, 0ull};   // diagnostics (flags & 8)
     for (int t = 0; t < 9; ++t) dA[t] = 0.f;
     dMu[0] = dMu[1] = dMu[2] = 0.f;
-#pragma unroll
-    for (int t = 0; t < kMaxK; ++t) dF[t] = 0.f;
     // this lane's Gaussian: record and feature row are re-read per wall point (L1/L2 hits) rather
     // than held in registers across the split (VGPR budget)
     const float* feat = k.g.features + (size_t)(active ? gi : 0) * k.g.k_feat;
@@ -996,6 +1011,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_B
             if (!anyact && !anypend) {
                 if (!anymore && qcount == 0) break;
                 continue;
+            }
+            if (NLOSGR_DIAG && (k.opt.flags & 8)) {
+                dg[0] += anyact ? 1u : 0u;
+                dg[1] += __popcll(__builtin_amdgcn_ballot_w64(act));
             }
             if (anyact) {
                 const int remw = act ? b.rem : 0;
@@ -1117,7 +1136,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_B
                             rV[r] = -(b.ts * zv + S1 * b.zs[r] + S2 * b.v[r]);
                         }
                         act = false;
-                        pend = true;
+                        pend = !(k.opt.flags & 32);   // flags 32 (diagnostics): drop results, no hand-off
                     }
                 }
             }
@@ -1146,12 +1165,18 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_B
                 dSig += gSig;
                 drho_pair += gRho;
                 wave_sync();
+                if (NLOSGR_DIAG && (k.opt.flags & 8)) {
+                    dg[2] += 1u;
+                    dg[3] += __popcll(__builtin_amdgcn_ballot_w64(pend));
+                    dg[4] += __popcll(__builtin_amdgcn_ballot_w64(won));
+                }
                 if (won) pend = false;
                 ++round;
             }
         }
-        // chain of this wall point's pair (Gaussian gi, wall point p): u0 = A (p - mu) and the
-        // SH view direction.  rho = max(0, 0.5 + sum_c f_c Y_c(dir)); w > 0 implies rho > 0.
+        // chain of this wall point's pair (Gaussian gi, wall point p) through u0 = A (p - mu); the
+        // view-direction chain through rho (SH basis, d_features and its d_mu share) runs in
+        // sh_kernel from the stored dL/drho, which keeps 16 feature accumulators out of this kernel
         if (active && wpair > 0.f) {
             const float q[3] = {px - mu[0], py - mu[1], pz - mu[2]};
             const float4* d4 = reinterpret_cast<const float4*>(pdat + lane * 16);
@@ -1160,42 +1185,74 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_B
             for (int r = 0; r < 3; ++r)
                 for (int cc = 0; cc < 3; ++cc) dA[3 * r + cc] += dU0p[r] * q[cc];
             for (int cc = 0; cc < 3; ++cc) dMu[cc] -= A[cc] * dU0p[0] + A[3 + cc] * dU0p[1] + A[6 + cc] * dU0p[2];
-            if (drho_pair != 0.f) {
-                float dir[3], nrm;
-                view_dir<PRESET>(-q[0], -q[1], -q[2], dir[0], dir[1], dir[2], nrm);
-                float Y[kMaxK];
-                sh_basis<PRESET>(deg, dir[0], dir[1], dir[2], Y);
-#pragma unroll
-                for (int cc = 0; cc < kMaxK; ++cc)
-                    if (cc < K) dF[cc] += drho_pair * Y[cc];
-                float gx, gy, gz;
-                sh_grad_dir<PRESET>(deg, dir[0], dir[1], dir[2], feat, gx, gy, gz);
-                float ox, oy, oz;
-                view_dir_bwd<PRESET>(-q[0], -q[1], -q[2], nrm, drho_pair * gx, drho_pair * gy, drho_pair * gz, ox,
-                                     oy, oz);
-                dMu[0] += ox; dMu[1] += oy; dMu[2] += oz;
-            }
         }
+        if (active) k.drho[(size_t)p * k.g.ng + gi] = (wpair > 0.f && !(k.opt.flags & 64)) ? drho_pair : 0.f;
     }
+    if (NLOSGR_DIAG && (k.opt.flags & 8) && k.counts && lane == 0)
+        for (int c = 0; c < 5; ++c) atomicAdd(k.counts + c, dg[c]);
     // fixed-order combination of the 4 waves' accumulators -> partial slab
     __syncthreads();
     float* red = smem + L.red;
     {
-        float* dst = red + (wave * 64 + lane) * 29;
+        float* dst = red + (wave * 64 + lane) * kBwdSlots;
         for (int t = 0; t < 9; ++t) dst[t] = dA[t];
         dst[9] = dMu[0]; dst[10] = dMu[1]; dst[11] = dMu[2];
         dst[12] = dSig;
-#pragma unroll
-        for (int t = 0; t < kMaxK; ++t) dst[13 + t] = dF[t];
     }
     __syncthreads();
-    for (int t = threadIdx.x; t < kNB * 29; t += blockDim.x) {
-        const int g = t / 29, c = t - g * 29;
+    for (int t = threadIdx.x; t < kNB * kBwdSlots; t += blockDim.x) {
+        const int g = t / kBwdSlots, c = t - g * kBwdSlots;
         if (gb + g >= k.g.ng) continue;
         float s = 0.f;
-        for (int w = 0; w < kWaves; ++w) s += red[(w * 64 + g) * 29 + c];
+        for (int w = 0; w < kWaves; ++w) s += red[(w * 64 + g) * kBwdSlots + c];
         k.partial[((size_t)split * k.g.ng + gb + g) * 32 + c] = s;
     }
+}
+
+// ------------------------------------------------------------------------------------------
+// sh_kernel: the view-direction chain of every pair from the backward's dL/drho (fixed wall-point
+// order within each of nsh splits): d_features += drho Y(dir), d_mu += drho (dY/ddir . f) ddir/dmu,
+// dir = view direction of mu - p (preset convention; nlos_helpers / cuda_utils.cuh semantics as in
+// the forward's pair_setup).  One lane per Gaussian; drho rows [P][ng] are read coalesced.
+// ------------------------------------------------------------------------------------------
+template <int PRESET>
+__global__ __launch_bounds__(kBlock) void sh_kernel(KArgs k) {
+    const int gi = blockIdx.x * blockDim.x + threadIdx.x;
+    if (gi >= k.g.ng) return;
+    const int split = blockIdx.y;
+    const int P_ = k.geo.nwall;
+    const int per = (P_ + k.nsh - 1) / k.nsh;
+    const int pbeg = split * per, pend = min(P_, pbeg + per);
+    const int deg = k.g.sh_degree;
+    const int K = (deg + 1) * (deg + 1);
+    const GaussRec rec = k.recs[gi];
+    const float mu[3] = {rec.a.x, rec.a.y, rec.a.z};
+    float f[kMaxK];
+    load_feat(k.g, gi, f);
+    float dF[kMaxK], dMu[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < kMaxK; ++c) dF[c] = 0.f;
+    for (int p = pbeg; p < pend; ++p) {
+        const float drho = k.drho[(size_t)p * k.g.ng + gi];
+        if (drho == 0.f) continue;
+        const float q[3] = {k.geo.wall[3 * p] - mu[0], k.geo.wall[3 * p + 1] - mu[1], k.geo.wall[3 * p + 2] - mu[2]};
+        float dir[3], nrm;
+        view_dir<PRESET>(-q[0], -q[1], -q[2], dir[0], dir[1], dir[2], nrm);
+        float Y[kMaxK];
+        sh_basis<PRESET>(deg, dir[0], dir[1], dir[2], Y);
+#pragma unroll
+        for (int c = 0; c < kMaxK; ++c)
+            if (c < K) dF[c] += drho * Y[c];
+        float gx, gy, gz;
+        sh_grad_dir<PRESET>(deg, dir[0], dir[1], dir[2], f, gx, gy, gz);
+        float ox, oy, oz;
+        view_dir_bwd<PRESET>(-q[0], -q[1], -q[2], nrm, drho * gx, drho * gy, drho * gz, ox, oy, oz);
+        dMu[0] += ox; dMu[1] += oy; dMu[2] += oz;
+    }
+    float* dst = k.shpart + ((size_t)split * k.g.ng + gi) * kShPart;
+#pragma unroll
+    for (int c = 0; c < kMaxK; ++c) dst[c] = dF[c];
+    dst[kMaxK] = dMu[0]; dst[kMaxK + 1] = dMu[1]; dst[kMaxK + 2] = dMu[2];
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1210,7 +1267,12 @@ __global__ __launch_bounds__(kBlock) void finish_kernel(KArgs k, float* d_mu, fl
     for (int t = 0; t < 32; ++t) acc[t] = 0.f;
     for (int s = 0; s < k.nsplit; ++s) {
         const float* src = k.partial + ((size_t)s * k.g.ng + i) * 32;
-        for (int t = 0; t < 29; ++t) acc[t] += src[t];
+        for (int t = 0; t < kBwdSlots; ++t) acc[t] += src[t];
+    }
+    for (int s = 0; s < k.nsh; ++s) {   // view-direction chain (sh_kernel)
+        const float* src = k.shpart + ((size_t)s * k.g.ng + i) * kShPart;
+        for (int t = 0; t < kMaxK; ++t) acc[13 + t] += src[t];
+        for (int t = 0; t < 3; ++t) acc[9 + t] += src[kMaxK + t];
     }
     chain_to_raw<PRESET>(k.g, i, acc, d_scaling, d_rot);
     d_mu[3 * i] = acc[9]; d_mu[3 * i + 1] = acc[10]; d_mu[3 * i + 2] = acc[11];
@@ -1337,6 +1399,19 @@ void dispatch_bwd(const KArgs& ka, bool dense, bool rays, size_t shm, hipStream_
 size_t cache_bytes(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_options* opt) {
     return opt->ray_cache ? align_up((size_t)geo->nwall * g->ng * 20) : 0;
 }
+// sh_kernel wall-point splits (>= 8 x 256-lane blocks per split row keep the chip busy at large Ng)
+int sh_nsplit(const nlosgr_gaussians* g, const nlosgr_geometry* geo) {
+    int ns = geo->nwall / 256;
+    const int nblk = (g->ng + kBlock - 1) / kBlock;
+    if (ns * nblk > 4096) ns = 4096 / (nblk > 0 ? nblk : 1);
+    if (ns > 64) ns = 64;
+    return ns < 1 ? 1 : ns;
+}
+// after the ray cache: drho [P][ng] | sh partials [nsh][ng][kShPart] | 256-B diagnostics tail
+size_t sh_bytes(const nlosgr_gaussians* g, const nlosgr_geometry* geo) {
+    return align_up((size_t)geo->nwall * g->ng * sizeof(float)) +
+           align_up((size_t)sh_nsplit(g, geo) * g->ng * kShPart * sizeof(float));
+}
 void cache_ptrs(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_options* opt, void* ws, int nsplit,
                 KArgs& ka) {
     if (!opt->ray_cache || g->ng == 0 || geo->nwall == 0) return;
@@ -1387,7 +1462,7 @@ size_t nlosgr_workspace_bytes(const nlosgr_gaussians* g, const nlosgr_geometry* 
     if (validate(g, geo, opt) != NLOSGR_OK) return 0;
     const size_t rec = align_up((size_t)g->ng * sizeof(GaussRec));
     const size_t part = align_up((size_t)bwd_nsplit(g, geo, opt) * g->ng * 32 * sizeof(float));
-    return rec + part + cache_bytes(g, geo, opt) + 256;
+    return rec + part + cache_bytes(g, geo, opt) + sh_bytes(g, geo) + 256;
 }
 
 int nlosgr_render_fwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_options* opt,
@@ -1430,6 +1505,17 @@ int nlosgr_render_bwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo, con
     ka.grad_hist = grad_hist; ka.grad_ray = grad_ray;
     ka.nsplit = bwd_nsplit(g, geo, opt);
     cache_ptrs(g, geo, opt, workspace, ka.nsplit, ka);
+    {
+        char* shb = (char*)workspace + align_up((size_t)g->ng * sizeof(GaussRec)) +
+                    align_up((size_t)ka.nsplit * g->ng * 32 * sizeof(float)) + cache_bytes(g, geo, opt);
+        ka.drho = (float*)shb;
+        ka.shpart = (float*)(shb + align_up((size_t)geo->nwall * g->ng * sizeof(float)));
+        ka.nsh = sh_nsplit(g, geo);
+        if (opt->flags & 8) {   // diagnostics: counters in the workspace's 256-B tail
+            ka.counts = (unsigned long long*)(shb + sh_bytes(g, geo));
+            HIPCHK(hipMemsetAsync(ka.counts, 0, 8 * sizeof(unsigned long long), s));
+        }
+    }
     launch_preprocess(g, (GaussRec*)workspace, s);
     HIPCHK(hipGetLastError());
     if (geo->nwall > 0 && (grad_hist || grad_ray)) {
@@ -1444,8 +1530,15 @@ int nlosgr_render_bwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo, con
             else dispatch_bwd<1, 1>(ka, dense, rays, shm, s);
         }
         HIPCHK(hipGetLastError());
+        const dim3 shgrid((g->ng + kBlock - 1) / kBlock, ka.nsh);
+        if (g->preset == NLOSGR_PRESET_TORCH)
+            hipLaunchKernelGGL(sh_kernel<NLOSGR_PRESET_TORCH>, shgrid, dim3(kBlock), 0, s, ka);
+        else
+            hipLaunchKernelGGL(sh_kernel<NLOSGR_PRESET_CUDA>, shgrid, dim3(kBlock), 0, s, ka);
+        HIPCHK(hipGetLastError());
     } else {
         HIPCHK(hipMemsetAsync(ka.partial, 0, (size_t)ka.nsplit * g->ng * 32 * sizeof(float), s));
+        ka.nsh = 0;
     }
     const int nb = (g->ng + kBlock - 1) / kBlock;
     if (g->preset == NLOSGR_PRESET_TORCH)

@@ -27,7 +27,7 @@ cache = os.environ.get("NLOSGR_ABLATE_CACHE", "1") == "1"
 hist, _, ws = render_forward(*args, base, ray_cache=True)
 grad = torch.randn_like(hist) * 1e-3
 bres = {}
-for flags in (0, 4, 1, 2):
+for flags in (0, 64, 32, 4, 1, 2):
     cfg = dataclasses.replace(base, flags=flags)
     kw = dict(workspace=ws, ray_cache=True) if cache else {}
     render_backward(*args, cfg, grad_hist=grad, **kw); torch.cuda.synchronize()
