@@ -64,6 +64,12 @@ using namespace nlosgr::detail;
 #ifndef NLOSGR_FREC
 #define NLOSGR_FREC 1          // forward no-occlusion drain: exp2 recurrence
 #endif
+#ifndef NLOSGR_BDECOUPLE
+#define NLOSGR_BDECOUPLE 0     // backward: lanes with a pending hand-off keep draining (measured slower: 409 vs 378 ms)
+#endif
+#ifndef NLOSGR_BDUAL
+#define NLOSGR_BDUAL 0         // backward hand-off: two claimants per pair and round (max / min lane; measured slower)
+#endif
 #ifndef NLOSGR_DIAG
 #define NLOSGR_DIAG 0          // utilisation counters under opt.flags 8 / 16 (scripts/drain_diag.py builds)
 #endif
@@ -730,7 +736,7 @@ constexpr int kBwdSlots = 13;   // per-Gaussian backward partial: dA[9], dMu[3],
 constexpr int kShPart = 20;     // sh_kernel partial: dF[16], dMu[3], pad
 
 struct BwdLayout {
-    int wave_base, wave_stride, grow, tth, tph, rayq, owner, pdat, red, total;
+    int wave_base, wave_stride, grow, tth, tph, rayq, owner, owner2, pdat, red, total;
     __host__ __device__ BwdLayout(int nr, int nt, int np_) {
         wave_base = 0;
         grow = 0;                            // [nr + kBSteps] upstream gradient x att x hscale, zero pad
@@ -738,7 +744,8 @@ struct BwdLayout {
         tph = tth + al4(2 * nt);             // float2 [np]
         rayq = tph + al4(2 * np_);           // uint [kRQ] ring
         owner = rayq + kRQ;                  // uint [64] round-stamped claims, indexed by pair slot
-        pdat = owner + 64;                   // [64][16] pair table: A[9], u0[3], w, rho, sigma, -
+        owner2 = owner + 64;                 // uint [64] second claim table (NLOSGR_BDUAL: min claim)
+        pdat = owner2 + (NLOSGR_BDUAL ? 64 : 0);   // [64][16] pair table: A[9], u0[3], w, rho, sigma, -
         wave_stride = al4(pdat + 64 * 16);
         red = wave_base;                     // final reduction reuses the wave regions
         total = wave_base + kWaves * wave_stride;
@@ -873,6 +880,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_B
     float2* tph = reinterpret_cast<float2*>(wb + L.tph);
     unsigned* rayq = reinterpret_cast<unsigned*>(wb + L.rayq);
     unsigned* owner = reinterpret_cast<unsigned*>(wb + L.owner);
+    unsigned* owner2 = reinterpret_cast<unsigned*>(wb + L.owner2);
     float* pdat = wb + L.pdat;
 
     const int gb = blockIdx.x * kNB;
@@ -925,7 +933,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_B
             for (int t = lane; t < np_; t += 64)
                 tph[t] = make_float2(k.geo.cos_phi[(size_t)p * np_ + t], k.geo.sin_phi[(size_t)p * np_ + t]);
         }
-        owner[lane] = 0xFFFFFFFFu;
+        owner[lane] = NLOSGR_BDUAL ? 0u : 0xFFFFFFFFu;
+        if (NLOSGR_BDUAL) owner2[lane] = 0xFFFFFFFFu;
         const float px = k.geo.wall[3 * p], py = k.geo.wall[3 * p + 1], pz = k.geo.wall[3 * p + 2];
         // pair setup (lane = Gaussian gi at wall point p); the ray pass reads the pair table
         bool more = false;
@@ -979,6 +988,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_B
         b.ph1 = false;
         // pending result of a finished ray: dL/du0, dL/dv, dsigma, drho
         float rU[3] = {0.f, 0.f, 0.f}, rV[3] = {0.f, 0.f, 0.f}, rSig = 0.f, rRho = 0.f;
+#if NLOSGR_BDECOUPLE
+        int pslot = lane, pij = 0;   // pair slot and ray of the pending result
+#else
+#define pslot b.slot
+#define pij b.ij
+#endif
         while (true) {
             if (CACHE && qcount < 64 && __builtin_amdgcn_ballot_w64((cbits0 | cbits1) != 0ull)) {
                 wave_sync();
@@ -991,11 +1006,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_B
                 wave_sync();
             }
             const bool anymore = __builtin_amdgcn_ballot_w64(more || (CACHE && (cbits0 | cbits1) != 0ull)) != 0;
-            const unsigned long long idle = __builtin_amdgcn_ballot_w64(!act && !pend);
+            // a lane whose finished result still waits for its hand-off keeps draining a new ray
+            // (NLOSGR_BDECOUPLE); it blocks only if that ray finishes first
+            const unsigned long long idle = __builtin_amdgcn_ballot_w64(!act && (NLOSGR_BDECOUPLE || !pend));
             const int nidle = __popcll(idle);
             if (qcount > 0 && (nidle >= kBRefill || !anymore)) {
                 const int r = lanes_below(idle);
-                const bool take = !act && !pend && r < qcount;
+                const bool take = !act && (NLOSGR_BDECOUPLE || !pend) && r < qcount;
                 if (take && !(k.opt.flags & 1)) {                  // flags 1: enumerate only
                     const unsigned e = rayq[(qhead + r) & (kRQ - 1)];
                     const int slot = e & 0xFF, i = (e >> 8) & 0xFFF, j = e >> 20;
@@ -1111,14 +1128,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_B
                     b.S0 = S0; b.S1 = S1; b.S2 = S2; b.dsig = dsig; b.drho = drho;
                 }
                 if (act) {
-                    b.kap = kap;
-                    b.pos += kBSteps;
-                    b.rem -= kBSteps;
-                    if (MODE == NLOSGR_MODE_NETF && b.rem <= 0 && !b.ph1) {   // second pass from the start
-                        b.ph1 = true;
-                        b.pos = b.kl; b.rem = b.len; b.kap = b.kap0; b.T = b.T0;
+                    if (b.rem > 0) {   // (a blocked lane, rem <= 0, added zeros and stays put)
+                        b.kap = kap;
+                        b.pos += kBSteps;
+                        b.rem -= kBSteps;
+                        if (MODE == NLOSGR_MODE_NETF && b.rem <= 0 && !b.ph1) {   // second pass from the start
+                            b.ph1 = true;
+                            b.pos = b.kl; b.rem = b.len; b.kap = b.kap0; b.T = b.T0;
+                        }
                     }
-                    if (b.rem <= 0) {
+                    if (b.rem <= 0 && !pend) {
                         // pdf = exp(-|z|^2/2), z = z* + dl v:  dL/du0 = -sum P z,  dL/dv = -sum P dl z
                         float S0 = b.S0, S1 = b.S1 * dr, S2 = b.S2 * dr * dr;
                         if (MODE == NLOSGR_MODE_NOOCL) {
@@ -1135,35 +1154,65 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_B
                             rU[r] = -zv;
                             rV[r] = -(b.ts * zv + S1 * b.zs[r] + S2 * b.v[r]);
                         }
+#if NLOSGR_BDECOUPLE
+                        pslot = b.slot;
+                        pij = b.ij;
+#endif
                         act = false;
                         pend = !(k.opt.flags & 32);   // flags 32 (diagnostics): drop results, no hand-off
                     }
                 }
             }
             if (__builtin_amdgcn_ballot_w64(pend)) {
-                // hand finished rays to their pair lanes (one claimant per pair per round)
-                const unsigned stamp = (round << 8) | (unsigned)lane;
-                if (pend) owner[b.slot] = stamp;
-                wave_sync();
-                const unsigned o = owner[lane];
-                const bool got = (o >> 8) == (round & 0xFFFFFFu);
-                const bool won = pend && owner[b.slot] == stamp;
-                const int src = got ? (int)(o & 63u) : lane;
-                const float gm = got ? 1.f : 0.f;
-                float gU[3], gV[3];
+                // hand finished rays to their pair lanes: per pair and round one claimant (or, with
+                // NLOSGR_BDUAL, the highest and the lowest claiming lane via LDS integer max / min)
+                bool won;
+                int srcs[2];
+                bool gots[2];
+                if (NLOSGR_BDUAL) {
+                    const unsigned sA = ((round + 1u) << 8) | (unsigned)lane;
+                    const unsigned sB = ((0xFFFFFEu - round) << 8) | (unsigned)lane;
+                    if (pend) {
+                        __hip_atomic_fetch_max(owner + pslot, sA, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        __hip_atomic_fetch_min(owner2 + pslot, sB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    }
+                    wave_sync();
+                    const unsigned oA = owner[lane], oB = owner2[lane];
+                    gots[0] = (oA >> 8) == ((round + 1u) & 0xFFFFFFu);
+                    gots[1] = (oB >> 8) == ((0xFFFFFEu - round) & 0xFFFFFFu) && (oB & 63u) != (oA & 63u);
+                    srcs[0] = gots[0] ? (int)(oA & 63u) : lane;
+                    srcs[1] = gots[1] ? (int)(oB & 63u) : lane;
+                    won = pend && (owner[pslot] == sA || owner2[pslot] == sB);
+                } else {
+                    const unsigned stamp = (round << 8) | (unsigned)lane;
+                    if (pend) owner[pslot] = stamp;
+                    wave_sync();
+                    const unsigned o = owner[lane];
+                    gots[0] = (o >> 8) == (round & 0xFFFFFFu);
+                    gots[1] = false;
+                    srcs[0] = gots[0] ? (int)(o & 63u) : lane;
+                    srcs[1] = lane;
+                    won = pend && owner[pslot] == stamp;
+                }
 #pragma unroll
-                for (int c = 0; c < 3; ++c) { gU[c] = gm * __shfl(rU[c], src); gV[c] = gm * __shfl(rV[c], src); }
-                const float gSig = gm * __shfl(rSig, src), gRho = gm * __shfl(rRho, src);
-                // every lane must execute the bpermute: it cannot read lanes that are inactive in EXEC
-                const int sij = __shfl(b.ij, src);
-                const int gij = got ? sij : 0;
-                const float2 th = tth[gij & 0xFFFF], ph = tph[gij >> 16];
-                const float d3[3] = {th.x * ph.x, th.x * ph.y, th.y};
-                for (int r = 0; r < 3; ++r)
-                    for (int c = 0; c < 3; ++c) dA[3 * r + c] += gV[r] * d3[c];
-                for (int r = 0; r < 3; ++r) dU0p[r] += gU[r];
-                dSig += gSig;
-                drho_pair += gRho;
+                for (int h = 0; h < (NLOSGR_BDUAL ? 2 : 1); ++h) {
+                    const int src = srcs[h];
+                    const float gm = gots[h] ? 1.f : 0.f;
+                    float gU[3], gV[3];
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) { gU[c] = gm * __shfl(rU[c], src); gV[c] = gm * __shfl(rV[c], src); }
+                    const float gSig = gm * __shfl(rSig, src), gRho = gm * __shfl(rRho, src);
+                    // every lane must execute the bpermute: it cannot read lanes that are inactive in EXEC
+                    const int sij = __shfl(pij, src);
+                    const int gij = gots[h] ? sij : 0;
+                    const float2 th = tth[gij & 0xFFFF], ph = tph[gij >> 16];
+                    const float d3[3] = {th.x * ph.x, th.x * ph.y, th.y};
+                    for (int r = 0; r < 3; ++r)
+                        for (int c = 0; c < 3; ++c) dA[3 * r + c] += gV[r] * d3[c];
+                    for (int r = 0; r < 3; ++r) dU0p[r] += gU[r];
+                    dSig += gSig;
+                    drho_pair += gRho;
+                }
                 wave_sync();
                 if (NLOSGR_DIAG && (k.opt.flags & 8)) {
                     dg[2] += 1u;
@@ -1174,6 +1223,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_B
                 ++round;
             }
         }
+#undef pslot
+#undef pij
         // chain of this wall point's pair (Gaussian gi, wall point p) through u0 = A (p - mu); the
         // view-direction chain through rho (SH basis, d_features and its d_mu share) runs in
         // sh_kernel from the stored dL/drho, which keeps 16 feature accumulators out of this kernel
