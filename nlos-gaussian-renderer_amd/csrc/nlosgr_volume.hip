@@ -579,6 +579,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_F
                 // b32 read-add-write is bank-conflict bound).  Slots before pos (first round of a
                 // segment only) add 0 and do not advance the recurrence, which starts at pos.
                 const int o = d.pos & 3;
+                const int lim = remw + o;   // slot j is in the segment iff o <= j < lim
                 float cur = fast_exp2(fmaf(d.ga, t * t, d.al));
                 float q = fast_exp2(d.ga * fmaf(2.f, t, 1.f));
                 const float cc = fast_exp2(2.f * d.ga);
@@ -591,11 +592,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_F
                         const int j = 4 * k4 + jj;
                         if (k4 == 0) {
                             const bool st = jj >= o;
-                            v[jj] = (st && j - o < remw) ? cur : 0.f;
+                            v[jj] = (st && j < lim) ? cur : 0.f;
                             cur = st ? cur * q : cur;
                             q = st ? q * cc : q;
                         } else {
-                            v[jj] = j - o < remw ? cur : 0.f;
+                            v[jj] = j < lim ? cur : 0.f;
                             cur *= q;
                             q *= cc;
                         }
