@@ -9,6 +9,9 @@ Layers:
     nlosgr.rendering_cuda  drop-in GaussianRendererCUDA / create_cuda_renderer / CUDA_AVAILABLE
     nlosgr.volume          full transient-volume render + MSE loss (the benchmarked step)
     nlosgr.distributed     relay-wall sharding over ranks + one all-reduce of Gaussian gradients
+    nlosgr.train           fused training iteration (nlosgr_mse + render fwd/bwd + nlosgr_adam)
+    nlosgr.data            Zaragoza capture format, data_shuffle, whole-volume targets / geometry
+    nlosgr.checkpoint      reference-keyed checkpoints loadable with weights_only=True
 """
 from . import _lib  # noqa: F401
 from .geometry import Geometry, build_geometry, relay_wall_grid, volume_box_point  # noqa: F401

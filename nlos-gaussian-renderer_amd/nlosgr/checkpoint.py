@@ -1,0 +1,68 @@
+"""Checkpoints with the reference's keys (GaussianModel.get_params / restore, gaussian_model.py:63-103;
+written by main.py's save_model) that load with torch.load(weights_only=True).
+
+The reference pickles the torch.optim.Adam object itself under 'optimizer', so its files only load
+with weights_only=False. Here 'optimizer' holds an Adam *state_dict* (plain tensors and numbers,
+the layout torch.optim.Adam.state_dict() produces for the six groups of gaussian_model.py:229-236),
+which the reference's restore accepts through its `load_state_dict(params['optimizer'])` branch,
+and which TrainStep reloads into its on-device Adam moments.
+"""
+import torch
+
+from .model import GaussianParams
+
+PARAM_KEYS = ("mu", "features_dc", "features_rest", "opacity", "scaling", "rotation")
+GROUP_ORDER = ("mu", "f_dc", "f_rest", "opacity", "scaling", "rotation")     # gaussian_model.py:229-236
+
+
+def _adam_state_dict(step):
+    """train.TrainStep's Adam as a torch.optim.Adam state_dict (group order of the reference)."""
+    adam = step.adam
+    lrs = step.learning_rates(step.iteration)
+    state, groups = {}, []
+    for i, name in enumerate(GROUP_ORDER):
+        p = adam.params[i]
+        state[i] = {"step": torch.tensor(float(adam.step_count)),
+                    "exp_avg": adam.exp_avg[i].detach().clone(),
+                    "exp_avg_sq": adam.exp_avg_sq[i].detach().clone()}
+        groups.append({"lr": float(lrs[i]), "betas": tuple(adam.betas), "eps": float(adam.eps), "weight_decay": 0.0,
+                       "amsgrad": False, "maximize": False, "foreach": None, "capturable": False,
+                       "differentiable": False, "fused": None, "name": name, "params": [i]})
+    return {"state": state, "param_groups": groups}
+
+
+def save_checkpoint(path, model, train_step=None):
+    """torch.save of {mu, features_dc, features_rest, opacity, scaling, rotation, optimizer,
+    max_sh_degree, active_sh_degree} (+ 'iteration' when a TrainStep is given)."""
+    ck = {k: getattr(model, "_" + k).detach().cpu() for k in PARAM_KEYS}
+    ck["max_sh_degree"] = int(model.max_sh_degree)
+    ck["active_sh_degree"] = int(model.active_sh_degree)
+    ck["optimizer"] = _adam_state_dict(train_step) if train_step is not None else None
+    if train_step is not None:
+        ck["iteration"] = int(train_step.iteration)
+    torch.save(ck, path)
+
+
+def load_checkpoint(path, device="cpu", train_step=None):
+    """GaussianParams from a checkpoint (weights_only=True: a reference file with a pickled optimizer
+    object is refused by torch; re-save it with the optimizer as a state_dict).  With train_step,
+    its parameters, Adam moments, step count and iteration are restored in place."""
+    ck = torch.load(path, map_location="cpu", weights_only=True)
+    t = {k: ck[k].float().to(device) for k in PARAM_KEYS}
+    model = GaussianParams(t["mu"], t["scaling"], t["rotation"], t["opacity"], t["features_dc"], t["features_rest"],
+                           int(ck["active_sh_degree"]), int(ck["max_sh_degree"]))
+    if train_step is not None:
+        m = train_step.model
+        with torch.no_grad():
+            for k in PARAM_KEYS:
+                getattr(m, "_" + k).data.copy_(t[k].to(m._mu.device))
+        m.active_sh_degree = int(ck["active_sh_degree"])
+        opt = ck.get("optimizer")
+        if opt:
+            for i in range(len(GROUP_ORDER)):
+                st = opt["state"][i]
+                train_step.adam.exp_avg[i].copy_(st["exp_avg"].reshape(train_step.adam.exp_avg[i].shape))
+                train_step.adam.exp_avg_sq[i].copy_(st["exp_avg_sq"].reshape(train_step.adam.exp_avg_sq[i].shape))
+            train_step.adam.step_count = int(float(opt["state"][0]["step"]))
+        train_step.iteration = int(ck.get("iteration", train_step.iteration))
+    return model

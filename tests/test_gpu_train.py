@@ -150,3 +150,30 @@ def test_train_step_matches_torch_composition(regularization):
     torch.cuda.synchronize()
     for n, a, b in zip(names, model.parameters(), twin.parameters()):
         assert _rel(a, b) <= 1e-5, n
+
+
+def test_train_step_checkpoint_resume(tmp_path):
+    """Two iterations, checkpoint, resume in a fresh TrainStep, one more iteration == three
+    uninterrupted iterations (Adam moments, step count and lr schedule restored)."""
+    from nlosgr import GaussianParams
+    from nlosgr.checkpoint import load_checkpoint, save_checkpoint
+    from nlosgr.train import TrainStep
+    dev = torch.device("cuda:0")
+    scene, model, geo, cfg, target = _scene_model(dev)
+    twin = GaussianParams(*(p.detach().clone() for p in model.parameters()), model.active_sh_degree)
+    a = TrainStep(model, geo, cfg, target, gt_times=100.0)
+    for _ in range(3):
+        a()
+    b = TrainStep(twin, geo, cfg, target, gt_times=100.0)
+    for _ in range(2):
+        b()
+    f = tmp_path / "ck.pt"
+    save_checkpoint(str(f), twin, b)
+    fresh = GaussianParams(*(torch.zeros_like(p) for p in twin.parameters()), 0, twin.max_sh_degree)
+    c = TrainStep(fresh, geo, cfg, target, gt_times=100.0)
+    load_checkpoint(str(f), dev, train_step=c)
+    assert c.iteration == 2 and c.adam.step_count == 2
+    c()
+    torch.cuda.synchronize()
+    for p, q in zip(model.parameters(), fresh.parameters()):
+        assert _rel(q, p) <= 1e-6
