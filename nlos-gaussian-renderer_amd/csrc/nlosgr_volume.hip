@@ -70,6 +70,9 @@ using namespace nlosgr::detail;
 #ifndef NLOSGR_BDUAL
 #define NLOSGR_BDUAL 0         // backward hand-off: two claimants per pair and round (max / min lane; measured slower)
 #endif
+#ifndef NLOSGR_BPEND
+#define NLOSGR_BPEND 1         // backward: run a hand-off round once this many lanes wait
+#endif
 #ifndef NLOSGR_DIAG
 #define NLOSGR_DIAG 0          // utilisation counters under opt.flags 8 / 16 (scripts/drain_diag.py builds)
 #endif
@@ -1164,7 +1167,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_B
                     }
                 }
             }
-            if (__builtin_amdgcn_ballot_w64(pend)) {
+            const unsigned long long pmask = __builtin_amdgcn_ballot_w64(pend);
+            // batch hand-offs: wait for NLOSGR_BPEND pending lanes unless nothing else can run
+            if (pmask && (__popcll(pmask) >= NLOSGR_BPEND || !__builtin_amdgcn_ballot_w64(act) ||
+                          (qcount == 0 && !anymore))) {
                 // hand finished rays to their pair lanes: per pair and round one claimant (or, with
                 // NLOSGR_BDUAL, the highest and the lowest claiming lane via LDS integer max / min)
                 bool won;
