@@ -79,6 +79,9 @@ using namespace nlosgr::detail;
 #ifndef NLOSGR_FQUAD
 #define NLOSGR_FQUAD 1         // forward culled no-occlusion drain: float4 read-add-write per 4 bins
 #endif
+#ifndef NLOSGR_FVEC
+#define NLOSGR_FVEC 2          // vector drain width: float2 (2) or float4 (4) read-add-write (C3 fwd 248 vs 282 ms)
+#endif
 #ifndef NLOSGR_BREC
 #define NLOSGR_BREC 1          // backward no-occlusion drain: exp2 recurrence + per-round moment sums
 #endif
@@ -293,10 +296,10 @@ __device__ __forceinline__ unsigned pack_ray(int slot, int i, int j) {
 // next round).  Lanes that did not win, or ran past their segment, point at private pad bins
 // and add 0, so the step body is branch-free.  Idle lanes are refilled from the ray queue.
 #ifndef NLOSGR_FSTEPS
-#define NLOSGR_FSTEPS 16
+#define NLOSGR_FSTEPS 24   // with the float2 drain: 24 bins per round (C3 fwd 238 vs 243 ms at 16, 261 at 32)
 #endif
 #ifndef NLOSGR_REFILL
-#define NLOSGR_REFILL 24
+#define NLOSGR_REFILL 32   // (C3: 16 -> 255, 24 -> 246, 32 -> 243, 40 -> 242, 48 -> 246 ms at 16 bins per round)
 #endif
 #ifndef NLOSGR_BREFILL
 #define NLOSGR_BREFILL 8
@@ -562,7 +565,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_F
             if (!anymore && qcount == 0 && have) break;   // next Gaussians; segments carry over
             // claim distinct start bins (quad drain: distinct start quads)
             constexpr bool QUAD = NLOSGR_FQUAD && NLOSGR_FREC && MODE == NLOSGR_MODE_NOOCL && !RAYS && !DENSE;
-            const int key = QUAD ? (d.pos >> 2) : d.pos;
+            constexpr int VW = NLOSGR_FVEC;   // bins per LDS read-add-write in the vector drain (4 or 2)
+            const int key = QUAD ? (d.pos / VW) : d.pos;
             if (act) owner[key] = (unsigned char)lane;
             wave_sync();
             const bool win = act && owner[key] == (unsigned char)lane;
@@ -573,7 +577,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_F
                 nseg += __popcll(__builtin_amdgcn_ballot_w64(act));
                 nsamp += __popcll(__builtin_amdgcn_ballot_w64(win));
             }
-            float* hb = hist + (win ? (QUAD ? (d.pos & ~3) : d.pos) : (QUAD ? padq : pad));
+            float* hb = hist + (win ? (QUAD ? (d.pos & ~(VW - 1)) : d.pos) : (QUAD ? padq : pad));
             float t = d.t;
             float logT = d.logT;
             float xlo = d.xlo, elo = d.elo;
@@ -581,19 +585,18 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_F
                 // 16 bins from the quad holding pos: one ds_read_b128 + ds_write_b128 per 4 bins (the
                 // b32 read-add-write is bank-conflict bound).  Slots before pos (first round of a
                 // segment only) add 0 and do not advance the recurrence, which starts at pos.
-                const int o = d.pos & 3;
+                const int o = d.pos & (VW - 1);
                 const int lim = remw + o;   // slot j is in the segment iff o <= j < lim
                 float cur = fast_exp2(fmaf(d.ga, t * t, d.al));
                 float q = fast_exp2(d.ga * fmaf(2.f, t, 1.f));
                 const float cc = fast_exp2(2.f * d.ga);
-                float4* hb4 = reinterpret_cast<float4*>(hb);
 #pragma unroll
-                for (int k4 = 0; k4 < kSteps / 4; ++k4) {
-                    float v[4];
+                for (int kv = 0; kv < kSteps / VW; ++kv) {
+                    float v[VW];
 #pragma unroll
-                    for (int jj = 0; jj < 4; ++jj) {
-                        const int j = 4 * k4 + jj;
-                        if (k4 == 0) {
+                    for (int jj = 0; jj < VW; ++jj) {
+                        const int j = VW * kv + jj;
+                        if (kv == 0) {
                             const bool st = jj >= o;
                             v[jj] = (st && j < lim) ? cur : 0.f;
                             cur = st ? cur * q : cur;
@@ -604,9 +607,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_F
                             q *= cc;
                         }
                     }
-                    float4 x = hb4[k4];
-                    x.x += v[0]; x.y += v[1]; x.z += v[2]; x.w += v[3];
-                    hb4[k4] = x;
+                    if (VW == 4) {
+                        float4* hb4 = reinterpret_cast<float4*>(hb);
+                        float4 x = hb4[kv];
+                        x.x += v[0]; x.y += v[1]; x.z += v[2]; x.w += v[VW - 1];
+                        hb4[kv] = x;
+                    } else {
+                        float2* hb2 = reinterpret_cast<float2*>(hb);
+                        float2 x = hb2[kv];
+                        x.x += v[0]; x.y += v[VW - 1];
+                        hb2[kv] = x;
+                    }
                     compiler_fence();
                 }
                 t += (float)(kSteps - o);
@@ -684,7 +695,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_F
                 compiler_fence();
             }
             if (win) {
-                const int adv = QUAD ? kSteps - (d.pos & 3) : kSteps;
+                const int adv = QUAD ? kSteps - (d.pos & (NLOSGR_FVEC - 1)) : kSteps;
                 d.t = t;
                 d.logT = logT;
                 d.xlo = xlo;
