@@ -376,26 +376,35 @@ __device__ __forceinline__ void enumerate_box(const float* M, int i1, int j0, in
                                               unsigned long long* rec1 = nullptr, int* cell = nullptr) {
     const int lane = lane_id();
     do {
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const float2 th = tth[min(ci, nt1)], ph = tph[cj];
-            const bool pass = more && (DENSE || quadric(M, th.x * ph.x, th.x * ph.y, th.y) >= 0.f);
-            if (REC) {   // cell index within the box (only boxes of <= 128 cells are cached)
-                const unsigned long long bit = 1ull << (*cell & 63);
-                *rec0 |= (pass && *cell < 64) ? bit : 0ull;
-                *rec1 |= (pass && (*cell >> 6) == 1) ? bit : 0ull;
-                *cell += 1;
-            }
-            const unsigned e = pack_ray(lane, ci, cj);
-            const bool wrap = cj >= j1;
-            cj = wrap ? j0 : cj + 1;
-            ci += wrap ? 1 : 0;
-            more = more && ci <= i1;
-            const unsigned long long m = __builtin_amdgcn_ballot_w64(pass);
-            if (pass) rayq[(qbase + cnt + lanes_below(m)) & (kRQ - 1)] = e;
-            cnt += __popcll(m);
-            if (NLOSGR_RQ_SMALL && cnt >= 64) return;
+        // two consecutive cells of the box (row-major): both table reads are issued before any
+        // queue store (an LDS store in between would order them), both tests are unpredicated
+        const bool wrapA = cj >= j1;
+        const int ciB = ci + (wrapA ? 1 : 0), cjB = wrapA ? j0 : cj + 1;
+        const bool moreB = more & (ciB <= i1);
+        const float2 thA = tth[min(ci, nt1)], phA = tph[cj];
+        const float2 thB = tth[min(ciB, nt1)], phB = tph[cjB];
+        const bool passA = more & (DENSE || quadric(M, thA.x * phA.x, thA.x * phA.y, thA.y) >= 0.f);
+        const bool passB = moreB & (DENSE || quadric(M, thB.x * phB.x, thB.x * phB.y, thB.y) >= 0.f);
+        if (REC) {   // cell index within the box (only boxes of <= 128 cells are cached)
+            const int c0 = *cell, c1 = c0 + 1;
+            *rec0 |= (passA & (c0 < 64)) ? (1ull << (c0 & 63)) : 0ull;
+            *rec1 |= (passA & ((c0 >> 6) == 1)) ? (1ull << (c0 & 63)) : 0ull;
+            *rec0 |= (passB & (c1 < 64)) ? (1ull << (c1 & 63)) : 0ull;
+            *rec1 |= (passB & ((c1 >> 6) == 1)) ? (1ull << (c1 & 63)) : 0ull;
+            *cell = c0 + 2;
         }
+        const unsigned eA = pack_ray(lane, ci, cj), eB = pack_ray(lane, ciB, cjB);
+        const bool wrapB = cjB >= j1;
+        cj = wrapB ? j0 : cjB + 1;
+        ci = ciB + (wrapB ? 1 : 0);
+        more = moreB & (ci <= i1);
+        const unsigned long long mA = __builtin_amdgcn_ballot_w64(passA);
+        const unsigned long long mB = __builtin_amdgcn_ballot_w64(passB);
+        const int nA = __popcll(mA);
+        if (passA) rayq[(qbase + cnt + lanes_below(mA)) & (kRQ - 1)] = eA;
+        if (passB) rayq[(qbase + cnt + nA + lanes_below(mB)) & (kRQ - 1)] = eB;
+        cnt += nA + __popcll(mB);
+        if (NLOSGR_RQ_SMALL && cnt >= 64) return;
     } while (cnt < 64 && __builtin_amdgcn_ballot_w64(more));
 }
 
