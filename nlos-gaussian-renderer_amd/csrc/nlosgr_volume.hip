@@ -73,6 +73,9 @@ using namespace nlosgr::detail;
 #ifndef NLOSGR_BPEND
 #define NLOSGR_BPEND 1         // backward: run a hand-off round once this many lanes wait
 #endif
+#ifndef NLOSGR_BVEC
+#define NLOSGR_BVEC 1          // backward no-occlusion drain: float2 reads of the gradient row
+#endif
 #ifndef NLOSGR_DIAG
 #define NLOSGR_DIAG 0          // utilisation counters under opt.flags 8 / 16 (scripts/drain_diag.py builds)
 #endif
@@ -755,7 +758,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_F
 // its pair: finished lanes claim owner[slot] with a round stamp, each pair lane gathers its
 // claimant's result with ds_bpermute and folds it into the Gaussian's register accumulators.
 // Losers keep their result and retry next round.  No LDS float atomics, no pair/row tables.
-constexpr int kBSteps = 16;
+#ifndef NLOSGR_BSTEPS
+#define NLOSGR_BSTEPS 24   // C3 bwd: 12 -> 396, 16 -> 375, 24 -> 355, 28 -> 376, 32 -> 383 ms (spills beyond 24)
+#endif
+constexpr int kBSteps = NLOSGR_BSTEPS;   // bins per lane per backward drain round
 constexpr int kBwdSlots = 13;   // per-Gaussian backward partial: dA[9], dMu[3], dsigma (stride 32 in HBM)
 constexpr int kShPart = 20;     // sh_kernel partial: dF[16], dMu[3], pad
 
@@ -1059,16 +1065,32 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_B
             }
             if (anyact) {
                 const int remw = act ? b.rem : 0;
-                const float* gr = grow + (act ? b.pos : 0);
+                // BV: the round starts at the even bin at or below pos (float2 row reads, half the LDS
+                // instructions); slot j is bin (pos & ~1) + j, in the segment iff o <= j < remw + o
+                constexpr bool BV = NLOSGR_BVEC && MODE == NLOSGR_MODE_NOOCL && !RAYS && !DENSE && NLOSGR_BREC &&
+                                    !NLOSGR_PACKED;
+                const int o = BV && act ? (b.pos & 1) : 0;
+                const float* gr = grow + (act ? b.pos - o : 0);
                 const float* gw = RAYS && gray ? gray + (size_t)((b.ij & 0xFFFF) * np_ + (b.ij >> 16)) * nr + b.pos
                                                : nullptr;
                 float Hs[kBSteps];
+                if (BV) {
+                    const int lim = remw + o;
+                    const float2* g2 = reinterpret_cast<const float2*>(gr);
 #pragma unroll
-                for (int m = 0; m < kBSteps; ++m) {
-                    float H = gr[m];
-                    if (RAYS || MODE == NLOSGR_MODE_NETF) H *= b.st;
-                    if (RAYS && gw && m < remw) H += gw[m] * rscale;
-                    Hs[m] = m < remw ? H : 0.f;
+                    for (int m = 0; m < kBSteps; m += 2) {
+                        const float2 h = g2[m / 2];
+                        Hs[m] = (m >= o && m < lim) ? h.x : 0.f;
+                        Hs[m + 1] = (m + 1 < lim) ? h.y : 0.f;
+                    }
+                } else {
+#pragma unroll
+                    for (int m = 0; m < kBSteps; ++m) {
+                        float H = gr[m];
+                        if (RAYS || MODE == NLOSGR_MODE_NETF) H *= b.st;
+                        if (RAYS && gw && m < remw) H += gw[m] * rscale;
+                        Hs[m] = m < remw ? H : 0.f;
+                    }
                 }
                 float kap = b.kap;
                 if (MODE == NLOSGR_MODE_NOOCL) {
@@ -1104,13 +1126,19 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_B
                             U0 += hp;
                             U1 = fmaf(hp, (float)m, U1);
                             U2 = fmaf(hp, (float)(m * m), U2);
-                            pdf *= q;
-                            q *= cc;
+                            if (BV && m == 0) {   // the recurrence starts at pos (slot o)
+                                pdf = o ? pdf : pdf * q;
+                                q = o ? q : q * cc;
+                            } else {
+                                pdf *= q;
+                                q *= cc;
+                            }
                         }
+                        const float kb = kap - (float)o;   // kap at slot 0
                         S0 += U0;
-                        S1 += fmaf(kap, U0, U1);
-                        S2 += fmaf(kap, fmaf(kap, U0, 2.f * U1), U2);
-                        kap += (float)kBSteps;
+                        S1 += fmaf(kb, U0, U1);
+                        S2 += fmaf(kb, fmaf(kb, U0, 2.f * U1), U2);
+                        kap += (float)(kBSteps - o);
                     } else
 #pragma unroll
                     for (int m = 0; m < kBSteps; ++m) {
@@ -1154,8 +1182,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_B
                 if (act) {
                     if (b.rem > 0) {   // (a blocked lane, rem <= 0, added zeros and stays put)
                         b.kap = kap;
-                        b.pos += kBSteps;
-                        b.rem -= kBSteps;
+                        b.pos += kBSteps - o;
+                        b.rem -= kBSteps - o;
                         if (MODE == NLOSGR_MODE_NETF && b.rem <= 0 && !b.ph1) {   // second pass from the start
                             b.ph1 = true;
                             b.pos = b.kl; b.rem = b.len; b.kap = b.kap0; b.T = b.T0;
