@@ -175,7 +175,7 @@ def main():
     bwd_avg = sum(bwd_ms) / len(bwd_ms) if bwd_ms else 0.0
     if bwd_avg >= fwd_avg:
         dom, dom_ms, dom_bytes = "bwd", bwd_avg, 2 * ng * pb + V
-        kern = ("preprocess_kernel", "bwd_kernel", "finish_kernel")
+        kern = ("preprocess_kernel", "bwd_kernel", "sh_kernel", "finish_kernel")
     else:
         dom, dom_ms, dom_bytes = "fwd", fwd_avg, ng * pb + V
         kern = ("preprocess_kernel", "fwd_kernel")
