@@ -1458,7 +1458,9 @@ int bwd_nsplit(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlos
     const int maxs = geo->nwall > 0 ? geo->nwall : 1;
     if (opt->nsplit > 0) return opt->nsplit < maxs ? opt->nsplit : maxs;
     const int nblk = (g->ng + kNB - 1) / kNB;
-    int ns = (2048 + nblk - 1) / (nblk > 0 ? nblk : 1);  // aim for >= 2048 workgroups (8 per CU)
+    // aim for ~48k workgroups: with 4 resident per CU a 3k-workgroup grid left a long last round
+    // (C3 backward: 2 splits 354 ms, 16 -> 309, 32 -> 305, 64 -> 302)
+    int ns = (49152 + nblk - 1) / (nblk > 0 ? nblk : 1);
     if (ns > maxs) ns = maxs;
     if (ns < 1) ns = 1;
     return ns;
