@@ -107,8 +107,10 @@ struct KArgs {
     unsigned long long* counts;  // optional [3]: pairs, segments, samples (nlosgr_count_support)
     ulonglong2* cmask;           // ray cache [P][ng]: passing rays of the pair's box (bit = box cell)
     float* drho;                 // backward: dL/drho per pair [P][ng] (0 outside the support) -> sh_kernel
+    float* hpart;                // forward Gaussian-split partial histograms [nfsplit][P][nr]
     float* shpart;               // sh_kernel partials [nsh][ng][kShPart]
     int nsh;                     // sh_kernel wall-point splits
+    int nfsplit;                 // forward Gaussian splits per wall point (hpart != null)
     unsigned* cbox;              // ray cache [P][ng]: i0 | j0 << 12 | width << 24, 0 = not cached
 };
 
@@ -448,6 +450,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_F
     unsigned char* owner = reinterpret_cast<unsigned char*>(wb + L.owner);
     unsigned* rayq = reinterpret_cast<unsigned*>(wb + L.rayq);
     const int p = blockIdx.x;
+    // Gaussian split of this wall point (grid.y; 64-aligned ranges): partial histograms are summed
+    // in split order by hist_reduce_kernel when gridDim.y > 1
+    const int gsplit = blockIdx.y, nsp = gridDim.y;
+    const int gper = (((k.g.ng + nsp - 1) / nsp) + 63) & ~63;
+    const int g_lo = gsplit * gper, g_hi = min(k.g.ng, g_lo + gper);
 
     for (int t = threadIdx.x; t < nt; t += blockDim.x)
         tth[t] = make_float2(k.geo.sin_theta[(size_t)p * nt + t], k.geo.cos_theta[(size_t)p * nt + t]);
@@ -485,13 +492,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_F
     GaussRec nrec;
     float nfeat[kMaxK];
     {
-        const int g0 = min(wave * 64 + lane, k.g.ng - 1);
+        const int g0 = min(g_lo + wave * 64 + lane, k.g.ng - 1);
         nrec = k.recs[g0];
         load_feat(k.g, g0, nfeat);
     }
 #endif
-    for (int base = wave * 64;; base += kBlock) {
-        const bool have = base < k.g.ng;      // wave-uniform
+    for (int base = g_lo + wave * 64;; base += kBlock) {
+        const bool have = base < g_hi;         // wave-uniform
         Pair P;
         float lw = 0.f, sc = 0.f, lwc = 0.f;
         bool more = false;
@@ -511,7 +518,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_F
                 load_feat(k.g, gl, nfeat);
             }
 #endif
-            if (gi < k.g.ng) {
+            if (gi < g_hi) {
                 float mu[3];
                 load_rec(nrec, P, mu);
                 pair_setup<PRESET, DENSE>(k, nfeat, mu, px, py, pz, lin, mc2, P);
@@ -526,7 +533,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_F
                 nsamp += more ? (unsigned)((P.i1 - P.i0 + 1) * (P.j1 - P.j0 + 1)) : 0u;
             ci = P.i0; cj = P.j0;
 #if NLOSGR_FWD_PF
-            if (base + kBlock < k.g.ng) {   // prefetch the next chunk
+            if (base + kBlock < g_hi) {   // prefetch the next chunk
                 const int gn = min(base + kBlock + lane, k.g.ng - 1);
                 nrec = k.recs[gn];
                 load_feat(k.g, gn, nfeat);
@@ -717,7 +724,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_F
                 act = d.rem > 0;
             }
         }
-        if (CACHE && have && base + lane < k.g.ng) {
+        if (CACHE && have && base + lane < g_hi) {
             // every candidate of this chunk has been tested: record the pair's passing cells
             const int bw = P.j1 - P.j0 + 1, bh = P.i1 - P.i0 + 1;
             const bool live = P.w > 0.f && bw > 0 && bh > 0;
@@ -744,9 +751,25 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_F
         for (int t = threadIdx.x; t < nr; t += blockDim.x) {
             float s = 0.f;
             for (int w = 0; w < kWaves; ++w) s += smem[w * L.wave_stride + L.hist + t];
-            k.hist_out[(size_t)p * nr + t] = s * k.geo.att[t] * hs;
+            if (nsp > 1)
+                k.hpart[((size_t)gsplit * k.geo.nwall + p) * nr + t] = s;
+            else
+                k.hist_out[(size_t)p * nr + t] = s * k.geo.att[t] * hs;
         }
     }
+}
+
+// forward Gaussian splits: hist[p,t] = (sum over splits in order) x att[t] x hscale[p]
+__global__ __launch_bounds__(kBlock) void hist_reduce_kernel(const float* __restrict__ hpart, int nsp, long long P,
+                                                             int nr, const float* __restrict__ att,
+                                                             const float* __restrict__ hscale, float* __restrict__ hist) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P * nr) return;
+    const long long p = i / nr;
+    const int t = (int)(i - p * nr);
+    float s = 0.f;
+    for (int sp = 0; sp < nsp; ++sp) s += hpart[(size_t)sp * P * nr + i];
+    hist[i] = s * att[t] * hscale[p];
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1469,7 +1492,8 @@ int bwd_nsplit(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlos
 
 template <int PRESET, int MODE, bool DENSE, bool RAYS, bool CACHE>
 void launch_fwd(const KArgs& ka, size_t shm, hipStream_t s) {
-    hipLaunchKernelGGL((fwd_kernel<PRESET, MODE, DENSE, RAYS, CACHE>), dim3(ka.geo.nwall), dim3(kBlock), shm, s, ka);
+    hipLaunchKernelGGL((fwd_kernel<PRESET, MODE, DENSE, RAYS, CACHE>), dim3(ka.geo.nwall, ka.hpart ? ka.nfsplit : 1),
+                       dim3(kBlock), shm, s, ka);
 }
 template <int PRESET, int MODE, bool DENSE, bool RAYS, bool CACHE>
 void launch_bwd(const KArgs& ka, size_t shm, hipStream_t s) {
@@ -1515,7 +1539,25 @@ int sh_nsplit(const nlosgr_gaussians* g, const nlosgr_geometry* geo) {
     if (ns > 64) ns = 64;
     return ns < 1 ? 1 : ns;
 }
-// after the ray cache: drho [P][ng] | sh partials [nsh][ng][kShPart] | 256-B diagnostics tail
+// forward Gaussian splits per wall point: aim for NLOSGR_FWG workgroups (a 16k-workgroup grid of
+// one long workgroup per wall point leaves a ragged last round), at least 256 Gaussians per split
+#ifndef NLOSGR_FWG
+#define NLOSGR_FWG 131072   // C3 fwd: 1 split 235 ms, 2 -> 232, 3 -> 231, 4 -> 230, 8 -> 229
+#endif
+int fwd_nsplit(const nlosgr_gaussians* g, const nlosgr_geometry* geo) {
+    if (geo->nwall <= 0) return 1;
+    int ns = (NLOSGR_FWG + geo->nwall - 1) / geo->nwall;
+    const int byg = (g->ng + 255) / 256;
+    if (ns > byg) ns = byg;
+    if (ns > 8) ns = 8;
+    return ns < 1 ? 1 : ns;
+}
+size_t fpart_bytes(const nlosgr_gaussians* g, const nlosgr_geometry* geo) {
+    const int ns = fwd_nsplit(g, geo);
+    return ns > 1 ? align_up((size_t)ns * geo->nwall * geo->nr * sizeof(float)) : 0;
+}
+// after the ray cache: drho [P][ng] | sh partials [nsh][ng][kShPart] | 256-B diagnostics tail |
+// forward split partial histograms [nfsplit][P][nr]
 size_t sh_bytes(const nlosgr_gaussians* g, const nlosgr_geometry* geo) {
     return align_up((size_t)geo->nwall * g->ng * sizeof(float)) +
            align_up((size_t)sh_nsplit(g, geo) * g->ng * kShPart * sizeof(float));
@@ -1538,6 +1580,13 @@ int run_fwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_
     ka.hist_out = hist_out; ka.ray_out = ray_out;
     ka.counts = counts;
     if (!counts) cache_ptrs(g, geo, opt, workspace, bwd_nsplit(g, geo, opt), ka);
+    const int nfs = fwd_nsplit(g, geo);
+    if (hist_out && nfs > 1 && g->ng > 0) {
+        ka.hpart = (float*)((char*)workspace + align_up((size_t)g->ng * sizeof(GaussRec)) +
+                            align_up((size_t)bwd_nsplit(g, geo, opt) * g->ng * 32 * sizeof(float)) +
+                            cache_bytes(g, geo, opt) + sh_bytes(g, geo) + 256);
+        ka.nfsplit = nfs;
+    }
     if (g->ng > 0) {
         launch_preprocess(g, (GaussRec*)workspace, s);
         HIPCHK(hipGetLastError());
@@ -1555,6 +1604,12 @@ int run_fwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_
         else dispatch_fwd<1, 2>(ka, dense, rays, shm, s);
     }
     HIPCHK(hipGetLastError());
+    if (ka.hpart) {
+        const long long n = (long long)geo->nwall * geo->nr;
+        hipLaunchKernelGGL(hist_reduce_kernel, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, ka.hpart,
+                           ka.nfsplit, (long long)geo->nwall, geo->nr, geo->att, geo->hscale, hist_out);
+        HIPCHK(hipGetLastError());
+    }
     return NLOSGR_OK;
 }
 
@@ -1570,7 +1625,7 @@ size_t nlosgr_workspace_bytes(const nlosgr_gaussians* g, const nlosgr_geometry* 
     if (validate(g, geo, opt) != NLOSGR_OK) return 0;
     const size_t rec = align_up((size_t)g->ng * sizeof(GaussRec));
     const size_t part = align_up((size_t)bwd_nsplit(g, geo, opt) * g->ng * 32 * sizeof(float));
-    return rec + part + cache_bytes(g, geo, opt) + sh_bytes(g, geo) + 256;
+    return rec + part + cache_bytes(g, geo, opt) + sh_bytes(g, geo) + 256 + fpart_bytes(g, geo);
 }
 
 int nlosgr_render_fwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_options* opt,
