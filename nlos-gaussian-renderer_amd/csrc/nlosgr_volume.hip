@@ -1030,7 +1030,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_B
         int ci = i0, cj = j0, qhead = 0, qcount = 0;
         unsigned round = 0;
         bool act = false, pend = false;
-        float dU0p[3] = {0.f, 0.f, 0.f}, drho_pair = 0.f;
+        float dU0p[3] = {0.f, 0.f, 0.f}, drho_pair = 0.f, s0_pair = 0.f;
         BRay b;
         b.pos = 0; b.rem = 0; b.slot = lane; b.ij = 0; b.kl = 0; b.len = 0;
         b.kap = b.kap0 = b.c0 = b.c2 = b.st = 0.f;
@@ -1217,8 +1217,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_B
                         float S0 = b.S0, S1 = b.S1 * dr, S2 = b.S2 * dr * dr;
                         if (MODE == NLOSGR_MODE_NOOCL) {
                             if (!RAYS) { S0 *= b.st; S1 *= b.st; S2 *= b.st; }
-                            rSig = S0 * b.rho;
-                            rRho = S0 * b.sigma;
+                            // no-occlusion: dsigma = S0 rho, drho = S0 sigma; the pair lane applies its own
+                            // rho and sigma to the summed S0 (one value handed over instead of two)
+                            rSig = S0;
+                            rRho = 0.f;
                             S0 *= b.w; S1 *= b.w; S2 *= b.w;
                         } else {
                             rSig = b.dsig;
@@ -1279,7 +1281,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_B
                     float gU[3], gV[3];
 #pragma unroll
                     for (int c = 0; c < 3; ++c) { gU[c] = gm * __shfl(rU[c], src); gV[c] = gm * __shfl(rV[c], src); }
-                    const float gSig = gm * __shfl(rSig, src), gRho = gm * __shfl(rRho, src);
+                    const float gSig = gm * __shfl(rSig, src);
+                    const float gRho = MODE == NLOSGR_MODE_NOOCL ? 0.f : gm * __shfl(rRho, src);
                     // every lane must execute the bpermute: it cannot read lanes that are inactive in EXEC
                     const int sij = __shfl(pij, src);
                     const int gij = gots[h] ? sij : 0;
@@ -1288,8 +1291,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_B
                     for (int r = 0; r < 3; ++r)
                         for (int c = 0; c < 3; ++c) dA[3 * r + c] += gV[r] * d3[c];
                     for (int r = 0; r < 3; ++r) dU0p[r] += gU[r];
-                    dSig += gSig;
-                    drho_pair += gRho;
+                    if (MODE == NLOSGR_MODE_NOOCL) {
+                        s0_pair += gSig;
+                    } else {
+                        dSig += gSig;
+                        drho_pair += gRho;
+                    }
                 }
                 wave_sync();
                 if (NLOSGR_DIAG && (k.opt.flags & 8)) {
@@ -1306,6 +1313,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_B
         // chain of this wall point's pair (Gaussian gi, wall point p) through u0 = A (p - mu); the
         // view-direction chain through rho (SH basis, d_features and its d_mu share) runs in
         // sh_kernel from the stored dL/drho, which keeps 16 feature accumulators out of this kernel
+        if (MODE == NLOSGR_MODE_NOOCL && active) {
+            const float4 wrs = reinterpret_cast<const float4*>(pdat + lane * 16)[3];   // w, rho, sigma
+            dSig += s0_pair * wrs.y;
+            drho_pair = s0_pair * wrs.z;
+        }
         if (active && wpair > 0.f) {
             const float q[3] = {px - mu[0], py - mu[1], pz - mu[2]};
             const float4* d4 = reinterpret_cast<const float4*>(pdat + lane * 16);
