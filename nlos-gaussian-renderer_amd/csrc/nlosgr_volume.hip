@@ -76,6 +76,10 @@ using namespace nlosgr::detail;
 #ifndef NLOSGR_BVEC
 #define NLOSGR_BVEC 1          // backward no-occlusion drain: float2 reads of the gradient row
 #endif
+#ifndef NLOSGR_BGLDS
+#define NLOSGR_BGLDS 0         // backward: gradient rows copied to LDS with global_load_lds (nr % 256 == 0;
+                               // measured 302 vs 298 ms at C3: the setup phase is not bound by the row staging)
+#endif
 #ifndef NLOSGR_DIAG
 #define NLOSGR_DIAG 0          // utilisation counters under opt.flags 8 / 16 (scripts/drain_diag.py builds)
 #endif
@@ -108,6 +112,7 @@ struct KArgs {
     ulonglong2* cmask;           // ray cache [P][ng]: passing rays of the pair's box (bit = box cell)
     float* drho;                 // backward: dL/drho per pair [P][ng] (0 outside the support) -> sh_kernel
     float* hpart;                // forward Gaussian-split partial histograms [nfsplit][P][nr]
+    const float* growall;        // backward: dL/dhist x att x hscale rows [P][nr] (grow_kernel), or null
     float* shpart;               // sh_kernel partials [nsh][ng][kShPart]
     int nsh;                     // sh_kernel wall-point splits
     int nfsplit;                 // forward Gaussian splits per wall point (hpart != null)
@@ -972,11 +977,24 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_B
                     ((reinterpret_cast<uintptr_t>(k.grad_hist) | reinterpret_cast<uintptr_t>(k.geo.att)) & 15) == 0;
     RowPF rpf;
     if (pf && pbeg + wave < pend) rpf.load(k, pbeg + wave, nr, nt, np_);
+    const bool glds = NLOSGR_BGLDS && k.growall != nullptr;   // host guarantees nr % 256 == 0
+    if (glds)
+        for (int t = nr + lane; t < nr + kBSteps; t += 64) grow[t] = 0.f;   // pad: never overwritten
     for (int p = pbeg + wave; p < pend; p += kWaves) {
         // stage this wall point's upstream gradient row and tables (wave-private)
         const float hs = k.geo.hscale[p];
         wave_sync();
-        if (pf) {
+        if (glds) {
+            // 1 KiB per wave-instruction straight into LDS; retired before the drain (s_waitcnt below)
+            const float* row = k.growall + (size_t)p * nr;
+            for (int c = 0; c < nr; c += 256)
+                __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(row + c + lane * 4),
+                                                 (__attribute__((address_space(3))) void*)(grow + c), 16, 0, 0);
+            for (int t = lane; t < nt; t += 64)
+                tth[t] = make_float2(k.geo.sin_theta[(size_t)p * nt + t], k.geo.cos_theta[(size_t)p * nt + t]);
+            for (int t = lane; t < np_; t += 64)
+                tph[t] = make_float2(k.geo.cos_phi[(size_t)p * np_ + t], k.geo.sin_phi[(size_t)p * np_ + t]);
+        } else if (pf) {
             rpf.store(k.geo.att, hs, nr, nt, np_, grow, tth, tph);
             if (p + kWaves < pend) rpf.load(k, p + kWaves, nr, nt, np_);
         } else {
@@ -1026,6 +1044,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_B
             }
         }
         const float* gray = RAYS && k.grad_ray ? k.grad_ray + (size_t)p * nt * np_ * nr : nullptr;
+        if (glds) __builtin_amdgcn_s_waitcnt(0);   // the row copy has landed in LDS
         wave_sync();
         int ci = i0, cj = j0, qhead = 0, qcount = 0;
         unsigned round = 0;
@@ -1350,6 +1369,18 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_B
     }
 }
 
+// grow_kernel: the backward's per-bin weights dL/dhist[p,k] att[k] hscale[p], once per wall point,
+// so bwd_kernel can copy rows straight into LDS (global_load_lds, no VGPR staging)
+__global__ __launch_bounds__(kBlock) void grow_kernel(const float* __restrict__ grad, const float* __restrict__ att,
+                                                      const float* __restrict__ hscale, long long P, int nr,
+                                                      float* __restrict__ out) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P * nr) return;
+    const long long p = i / nr;
+    const int t = (int)(i - p * nr);
+    out[i] = grad[i] * att[t] * hscale[p];
+}
+
 // ------------------------------------------------------------------------------------------
 // sh_kernel: the view-direction chain of every pair from the backward's dL/drho (fixed wall-point
 // order within each of nsh splits): d_features += drho Y(dir), d_mu += drho (dY/ddir . f) ddir/dmu,
@@ -1637,7 +1668,8 @@ size_t nlosgr_workspace_bytes(const nlosgr_gaussians* g, const nlosgr_geometry* 
     if (validate(g, geo, opt) != NLOSGR_OK) return 0;
     const size_t rec = align_up((size_t)g->ng * sizeof(GaussRec));
     const size_t part = align_up((size_t)bwd_nsplit(g, geo, opt) * g->ng * 32 * sizeof(float));
-    return rec + part + cache_bytes(g, geo, opt) + sh_bytes(g, geo) + 256 + fpart_bytes(g, geo);
+    return rec + part + cache_bytes(g, geo, opt) + sh_bytes(g, geo) + 256 + fpart_bytes(g, geo) +
+           (NLOSGR_BGLDS ? align_up((size_t)geo->nwall * geo->nr * sizeof(float)) : 0);   // grow_kernel rows
 }
 
 int nlosgr_render_fwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_options* opt,
@@ -1686,6 +1718,14 @@ int nlosgr_render_bwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo, con
         ka.drho = (float*)shb;
         ka.shpart = (float*)(shb + align_up((size_t)geo->nwall * g->ng * sizeof(float)));
         ka.nsh = sh_nsplit(g, geo);
+        if (NLOSGR_BGLDS && grad_hist && geo->nwall > 0 && (geo->nr % 256) == 0) {
+            float* rows = (float*)(shb + sh_bytes(g, geo) + 256 + fpart_bytes(g, geo));
+            const long long n = (long long)geo->nwall * geo->nr;
+            hipLaunchKernelGGL(grow_kernel, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, grad_hist,
+                               geo->att, geo->hscale, (long long)geo->nwall, geo->nr, rows);
+            HIPCHK(hipGetLastError());
+            ka.growall = rows;
+        }
         if (opt->flags & 8) {   // diagnostics: counters in the workspace's 256-B tail
             ka.counts = (unsigned long long*)(shb + sh_bytes(g, geo));
             HIPCHK(hipMemsetAsync(ka.counts, 0, 8 * sizeof(unsigned long long), s));
