@@ -80,6 +80,9 @@ using namespace nlosgr::detail;
 #define NLOSGR_BGLDS 0         // backward: gradient rows copied to LDS with global_load_lds (nr % 256 == 0;
                                // measured 302 vs 298 ms at C3: the setup phase is not bound by the row staging)
 #endif
+#ifndef NLOSGR_BRHO
+#define NLOSGR_BRHO 1          // ray cache also records each pair's albedo: the backward skips SH / footprint
+#endif
 #ifndef NLOSGR_DIAG
 #define NLOSGR_DIAG 0          // utilisation counters under opt.flags 8 / 16 (scripts/drain_diag.py builds)
 #endif
@@ -117,6 +120,7 @@ struct KArgs {
     int nsh;                     // sh_kernel wall-point splits
     int nfsplit;                 // forward Gaussian splits per wall point (hpart != null)
     unsigned* cbox;              // ray cache [P][ng]: i0 | j0 << 12 | width << 24, 0 = not cached
+    float* crho;                 // ray cache [P][ng]: the pair's SH albedo rho (NLOSGR_BRHO)
 };
 
 // ray cache: a pair whose (theta, phi) candidate box has at most 128 cells records which cells
@@ -737,6 +741,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_F
             const bool ok = !live || bw * bh <= kCacheCells;
             k.cmask[o] = live ? make_ulonglong2(crec0, crec1) : make_ulonglong2(0ull, 0ull);
             k.cbox[o] = ok ? cache_box(live ? P.i0 : 0, live ? P.j0 : 0, live ? bw : 1) : 0u;
+            if (NLOSGR_BRHO) k.crho[o] = live ? P.rho : 0.f;
         }
         if (!have) break;
     }
@@ -1012,11 +1017,25 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_B
         float M[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
         int i0 = 0, i1 = -1, j0 = 0, j1 = -1;
         float wpair = 0.f;
+        unsigned bx = 0u;
         if (active) {
             Pair P;
             float mu_[3];
             load_rec(k.recs[gi], P, mu_);
-            pair_setup<PRESET, DENSE>(k, feat, mu, px, py, pz, k.geo.grid_lin + 4 * (size_t)p, mc2, P);
+            if (CACHE) bx = k.cbox[(size_t)p * k.g.ng + gi];
+            if (CACHE && NLOSGR_BRHO && bx != 0u) {
+                // cached pair: u0 and the forward's albedo; no SH evaluation, no footprint (the
+                // recorded cells replace the quadric walk)
+                P.q[0] = px - mu[0]; P.q[1] = py - mu[1]; P.q[2] = pz - mu[2];
+                for (int r = 0; r < 3; ++r)
+                    P.u0[r] = P.A[3 * r] * P.q[0] + P.A[3 * r + 1] * P.q[1] + P.A[3 * r + 2] * P.q[2];
+                P.rho = k.crho[(size_t)p * k.g.ng + gi];
+                P.w = P.sigma * P.rho;
+                P.i0 = P.j0 = 0; P.i1 = P.j1 = 0;
+                for (int t = 0; t < 6; ++t) P.M[t] = 0.f;
+            } else {
+                pair_setup<PRESET, DENSE>(k, feat, mu, px, py, pz, k.geo.grid_lin + 4 * (size_t)p, mc2, P);
+            }
             more = (P.w > 0.f) && P.i0 <= P.i1 && P.j0 <= P.j1 && !(k.opt.flags & 2);  // flags 2: setup only
             for (int t = 0; t < 6; ++t) M[t] = P.M[t];
             i0 = P.i0; i1 = P.i1; j0 = P.j0; j1 = P.j1;
@@ -1033,7 +1052,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_B
         float rcw = 1.f;
         if (CACHE && active) {
             const size_t o = (size_t)p * k.g.ng + gi;
-            const unsigned bx = k.cbox[o];
             if (bx != 0u) {
                 const ulonglong2 cm = k.cmask[o];
                 cbits0 = more ? cm.x : 0ull;
@@ -1572,7 +1590,7 @@ void dispatch_bwd(const KArgs& ka, bool dense, bool rays, size_t shm, hipStream_
 // workspace layout: GaussRec[ng] | backward partials [nsplit][ng][32] | ray cache (opt->ray_cache):
 // mask 2 x u64 [P][ng] | box u32 [P][ng]
 size_t cache_bytes(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_options* opt) {
-    return opt->ray_cache ? align_up((size_t)geo->nwall * g->ng * 20) : 0;
+    return opt->ray_cache ? align_up((size_t)geo->nwall * g->ng * (NLOSGR_BRHO ? 24 : 20)) : 0;
 }
 // sh_kernel wall-point splits (>= 8 x 256-lane blocks per split row keep the chip busy at large Ng)
 int sh_nsplit(const nlosgr_gaussians* g, const nlosgr_geometry* geo) {
@@ -1611,6 +1629,7 @@ void cache_ptrs(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlo
     char* base = (char*)ws + align_up((size_t)g->ng * sizeof(GaussRec)) + align_up((size_t)nsplit * g->ng * 32 * sizeof(float));
     ka.cmask = (ulonglong2*)base;
     ka.cbox = (unsigned*)(base + (size_t)geo->nwall * g->ng * 16);
+    ka.crho = (float*)(base + (size_t)geo->nwall * g->ng * 20);
 }
 
 int run_fwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_options* opt, void* workspace,

@@ -15,7 +15,7 @@ import torch
 
 from . import _lib
 
-# upper bound on the forward->backward ray cache (20 B per wall point x Gaussian pair; C3: 33 GB)
+# upper bound on the forward->backward ray cache (24 B per wall point x Gaussian pair; C3: 39 GB)
 RAY_CACHE_MAX_BYTES = int(float(os.environ.get("NLOSGR_RAY_CACHE_GB", "96")) * 2 ** 30)
 
 
@@ -36,7 +36,7 @@ class RenderConfig:
 def use_ray_cache(cfg, geo, ng, want_rays=False):
     """The forward->backward ray cache applies to culled, histogram-only, differentiable modes."""
     return (bool(cfg.ray_cache) and cfg.cutoff > 0 and not want_rays and cfg.mode in ("noocl", "netf")
-            and geo.nwall * ng * 20 <= RAY_CACHE_MAX_BYTES)
+            and geo.nwall * ng * 24 <= RAY_CACHE_MAX_BYTES)
 
 
 def _as_f32(t):
