@@ -83,6 +83,9 @@ using namespace nlosgr::detail;
 #ifndef NLOSGR_BRHO
 #define NLOSGR_BRHO 1          // ray cache also records each pair's albedo: the backward skips SH / footprint
 #endif
+#ifndef NLOSGR_BSENDD
+#define NLOSGR_BSENDD 0        // backward hand-off: send the ray direction (3 bpermutes) instead of its cell (slower: 290 vs 284 ms)
+#endif
 #ifndef NLOSGR_DIAG
 #define NLOSGR_DIAG 0          // utilisation counters under opt.flags 8 / 16 (scripts/drain_diag.py builds)
 #endif
@@ -1078,6 +1081,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_B
         b.ph1 = false;
         // pending result of a finished ray: dL/du0, dL/dv, dsigma, drho
         float rU[3] = {0.f, 0.f, 0.f}, rV[3] = {0.f, 0.f, 0.f}, rSig = 0.f, rRho = 0.f;
+        float rD[3] = {0.f, 0.f, 0.f};   // NLOSGR_BSENDD: the finished ray's direction
 #if NLOSGR_BDECOUPLE
         int pslot = lane, pij = 0;   // pair slot and ray of the pending result
 #else
@@ -1268,6 +1272,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_B
                             rU[r] = -zv;
                             rV[r] = -(b.ts * zv + S1 * b.zs[r] + S2 * b.v[r]);
                         }
+                        if (NLOSGR_BSENDD) {   // the ray direction travels with the result
+                            const float2 th = tth[b.ij & 0xFFFF], ph = tph[b.ij >> 16];
+                            rD[0] = th.x * ph.x; rD[1] = th.x * ph.y; rD[2] = th.y;
+                        }
 #if NLOSGR_BDECOUPLE
                         pslot = b.slot;
                         pij = b.ij;
@@ -1321,10 +1329,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_B
                     const float gSig = gm * __shfl(rSig, src);
                     const float gRho = MODE == NLOSGR_MODE_NOOCL ? 0.f : gm * __shfl(rRho, src);
                     // every lane must execute the bpermute: it cannot read lanes that are inactive in EXEC
-                    const int sij = __shfl(pij, src);
-                    const int gij = gots[h] ? sij : 0;
-                    const float2 th = tth[gij & 0xFFFF], ph = tph[gij >> 16];
-                    const float d3[3] = {th.x * ph.x, th.x * ph.y, th.y};
+                    float d3[3];
+                    if (NLOSGR_BSENDD) {
+#pragma unroll
+                        for (int c = 0; c < 3; ++c) d3[c] = __shfl(rD[c], src);
+                    } else {
+                        const int sij = __shfl(pij, src);
+                        const int gij = gots[h] ? sij : 0;
+                        const float2 th = tth[gij & 0xFFFF], ph = tph[gij >> 16];
+                        d3[0] = th.x * ph.x; d3[1] = th.x * ph.y; d3[2] = th.y;
+                    }
                     for (int r = 0; r < 3; ++r)
                         for (int c = 0; c < 3; ++c) dA[3 * r + c] += gV[r] * d3[c];
                     for (int r = 0; r < 3; ++r) dU0p[r] += gU[r];
