@@ -20,6 +20,7 @@
  *                          main.py:203-213 (torch.optim.Adam groups, gaussian_model.py:223-242)
  *   nlosgr_bboxes       <- compute_gaussian_bboxes_kernel include/bbox_compute.cuh:76-120,
  *                          GaussianModel.get_bboxes gaussian_model/gaussian_model.py:140-178
+ *   nlosgr_carve_votes  <- the voting loop of space_carving gaussian_model/gaussian_utils.py:88-99
  */
 #ifndef NLOSGR_H
 #define NLOSGR_H
@@ -37,7 +38,7 @@
 extern "C" {
 #endif
 
-#define NLOSGR_ABI_VERSION 2
+#define NLOSGR_ABI_VERSION 3
 
 /* convention presets */
 enum {
@@ -223,6 +224,15 @@ NLOSGR_API int nlosgr_mse(const float* hist, const float* target, float gt_times
  * uses betas (0.9, 0.999), eps 1e-15 and six groups (gaussian_model.py:223-242). */
 NLOSGR_API int nlosgr_adam(const nlosgr_adam_group* groups, int32_t ngroups, long long step, double beta1,
                 double beta2, double eps, void* hip_stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Space-carving initialisation.  votes[v] (v < nvox) = number of wall points i
+ * with radius[i] > 0 and |coords[v] - walls[i]| >= radius[i] (fp32, torch.norm order, no fma):
+ * the voting loop of space_carving (gaussian_utils.py:88-99).  coords [nvox][3], walls [nwall][3]
+ * and radius [nwall] are device arrays in the same frame; votes [nvox] int32 is overwritten.
+ * ------------------------------------------------------------------------------------- */
+NLOSGR_API int nlosgr_carve_votes(const float* coords, long long nvox, const float* walls, const float* radius,
+                       int32_t nwall, int32_t* votes, void* hip_stream);
 
 NLOSGR_API const char* nlosgr_last_error(void);
 NLOSGR_API int nlosgr_abi_version(void);

@@ -54,13 +54,13 @@ class AdamGroup(ctypes.Structure):
 
 ADAM_MAX_GROUPS = 8  # NLOSGR_ADAM_MAX_GROUPS
 MAX_PER_RAY = 256   # NLOSGR_MAX_PER_RAY
-ABI_VERSION = 2     # NLOSGR_ABI_VERSION
+ABI_VERSION = 3     # NLOSGR_ABI_VERSION
 
 # every symbol include/nlosgr.h declares (tests check the exports against this list)
 EXPORTS = ["nlosgr_workspace_bytes", "nlosgr_render_fwd", "nlosgr_render_bwd", "nlosgr_count_support",
            "nlosgr_bboxes", "nlosgr_rays_workspace_bytes", "nlosgr_filter_rays", "nlosgr_rays_fwd",
            "nlosgr_rays_bwd", "nlosgr_rays_analytic", "nlosgr_mse_workspace_bytes", "nlosgr_mse", "nlosgr_adam",
-           "nlosgr_last_error", "nlosgr_abi_version"]
+           "nlosgr_carve_votes", "nlosgr_last_error", "nlosgr_abi_version"]
 
 _lib = None
 _load_error = None
@@ -103,6 +103,8 @@ def load():
     lib.nlosgr_adam.argtypes = [ctypes.POINTER(AdamGroup), ctypes.c_int32, ctypes.c_longlong, ctypes.c_double,
                                 ctypes.c_double, ctypes.c_double, _P]
     lib.nlosgr_adam.restype = ctypes.c_int
+    lib.nlosgr_carve_votes.argtypes = [_P, ctypes.c_longlong, _P, _P, ctypes.c_int32, _P, _P]
+    lib.nlosgr_carve_votes.restype = ctypes.c_int
     lib.nlosgr_bboxes.argtypes = [PG, ctypes.c_float, _P, _P]
     lib.nlosgr_bboxes.restype = ctypes.c_int
     lib.nlosgr_last_error.argtypes = []
