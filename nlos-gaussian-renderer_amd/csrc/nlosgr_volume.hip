@@ -386,41 +386,64 @@ __device__ __forceinline__ bool drain_setup(const float* A, const float* u0, flo
 // to the ray queue ring at qbase + cnt.  Branch-free body (every lane evaluates a clamped
 // candidate, `more` masks the result), two candidates per trip so their table reads overlap;
 // returns once cnt >= 64 or every lane exhausted its box (cnt < 64 + 2*64 <= kRQ on return).
+#ifndef NLOSGR_ENUM_NC
+#define NLOSGR_ENUM_NC 3       // candidate cells per enumeration trip (<= 3: cnt < 64 + NC*64 <= kRQ; C3 fwd 1: 234, 2: 229, 3: 227 ms)
+#endif
 template <bool DENSE, bool REC = false>
 __device__ __forceinline__ void enumerate_box(const float* M, int i1, int j0, int j1, bool& more, int& ci, int& cj,
                                               const float2* tth, const float2* tph, int nt1, unsigned* rayq,
                                               int qbase, int& cnt, unsigned long long* rec0 = nullptr,
                                               unsigned long long* rec1 = nullptr, int* cell = nullptr) {
+    constexpr int NC = NLOSGR_ENUM_NC;
+    static_assert(NC >= 1 && 64 + NC * 64 <= kRQ, "enumeration would overflow the ray queue ring");
     const int lane = lane_id();
     do {
-        // two consecutive cells of the box (row-major): both table reads are issued before any
-        // queue store (an LDS store in between would order them), both tests are unpredicated
-        const bool wrapA = cj >= j1;
-        const int ciB = ci + (wrapA ? 1 : 0), cjB = wrapA ? j0 : cj + 1;
-        const bool moreB = more & (ciB <= i1);
-        const float2 thA = tth[min(ci, nt1)], phA = tph[cj];
-        const float2 thB = tth[min(ciB, nt1)], phB = tph[cjB];
-        const bool passA = more & (DENSE || quadric(M, thA.x * phA.x, thA.x * phA.y, thA.y) >= 0.f);
-        const bool passB = moreB & (DENSE || quadric(M, thB.x * phB.x, thB.x * phB.y, thB.y) >= 0.f);
-        if (REC) {   // cell index within the box (only boxes of <= 128 cells are cached)
-            const int c0 = *cell, c1 = c0 + 1;
-            *rec0 |= (passA & (c0 < 64)) ? (1ull << (c0 & 63)) : 0ull;
-            *rec1 |= (passA & ((c0 >> 6) == 1)) ? (1ull << (c0 & 63)) : 0ull;
-            *rec0 |= (passB & (c1 < 64)) ? (1ull << (c1 & 63)) : 0ull;
-            *rec1 |= (passB & ((c1 >> 6) == 1)) ? (1ull << (c1 & 63)) : 0ull;
-            *cell = c0 + 2;
+        // NC consecutive cells of the box (row-major): all table reads are issued before any queue
+        // store (an LDS store in between would order them), the tests are unpredicated
+        int cis[NC], cjs[NC];
+        bool mores[NC];
+        cis[0] = ci; cjs[0] = cj; mores[0] = more;
+#pragma unroll
+        for (int u = 1; u < NC; ++u) {
+            const bool wrap = cjs[u - 1] >= j1;
+            cis[u] = cis[u - 1] + (wrap ? 1 : 0);
+            cjs[u] = wrap ? j0 : cjs[u - 1] + 1;
+            mores[u] = mores[u - 1] & (cis[u] <= i1);
         }
-        const unsigned eA = pack_ray(lane, ci, cj), eB = pack_ray(lane, ciB, cjB);
-        const bool wrapB = cjB >= j1;
-        cj = wrapB ? j0 : cjB + 1;
-        ci = ciB + (wrapB ? 1 : 0);
-        more = moreB & (ci <= i1);
-        const unsigned long long mA = __builtin_amdgcn_ballot_w64(passA);
-        const unsigned long long mB = __builtin_amdgcn_ballot_w64(passB);
-        const int nA = __popcll(mA);
-        if (passA) rayq[(qbase + cnt + lanes_below(mA)) & (kRQ - 1)] = eA;
-        if (passB) rayq[(qbase + cnt + nA + lanes_below(mB)) & (kRQ - 1)] = eB;
-        cnt += nA + __popcll(mB);
+        float2 ths[NC], phs[NC];
+#pragma unroll
+        for (int u = 0; u < NC; ++u) { ths[u] = tth[min(cis[u], nt1)]; phs[u] = tph[cjs[u]]; }
+        bool pass[NC];
+#pragma unroll
+        for (int u = 0; u < NC; ++u)
+            pass[u] = mores[u] & (DENSE || quadric(M, ths[u].x * phs[u].x, ths[u].x * phs[u].y, ths[u].y) >= 0.f);
+        if (REC) {   // cell index within the box (only boxes of <= 128 cells are cached)
+            const int c0 = *cell;
+#pragma unroll
+            for (int u = 0; u < NC; ++u) {
+                const int cu = c0 + u;
+                *rec0 |= (pass[u] & (cu < 64)) ? (1ull << (cu & 63)) : 0ull;
+                *rec1 |= (pass[u] & ((cu >> 6) == 1)) ? (1ull << (cu & 63)) : 0ull;
+            }
+            *cell = c0 + NC;
+        }
+        unsigned es[NC];
+#pragma unroll
+        for (int u = 0; u < NC; ++u) es[u] = pack_ray(lane, cis[u], cjs[u]);
+        {
+            const bool wrap = cjs[NC - 1] >= j1;
+            cj = wrap ? j0 : cjs[NC - 1] + 1;
+            ci = cis[NC - 1] + (wrap ? 1 : 0);
+            more = mores[NC - 1] & (ci <= i1);
+        }
+        int at = cnt;
+#pragma unroll
+        for (int u = 0; u < NC; ++u) {
+            const unsigned long long m = __builtin_amdgcn_ballot_w64(pass[u]);
+            if (pass[u]) rayq[(qbase + at + lanes_below(m)) & (kRQ - 1)] = es[u];
+            at += __popcll(m);
+        }
+        cnt = at;
         if (NLOSGR_RQ_SMALL && cnt >= 64) return;
     } while (cnt < 64 && __builtin_amdgcn_ballot_w64(more));
 }
