@@ -133,6 +133,22 @@ class TrainStep:
                          model._opacity.data.view(ng), model._scaling.data, model._rotation.data]
         self.adam = Adam(self._tensors, eps=1e-15)
 
+    def rebind(self, exp_avg=None, exp_avg_sq=None):
+        """Re-point the step at the model's (possibly resized) parameter tensors after density control
+        (nlosgr.densify); the Adam moments are replaced by the given lists (group order of GROUPS) and
+        the step count is kept."""
+        m = self.model
+        ng = m._mu.shape[0]
+        self._tensors = [m._mu.data, m._features_dc.data.view(ng, -1), m._features_rest.data.view(ng, -1),
+                         m._opacity.data.view(ng), m._scaling.data, m._rotation.data]
+        step_count = self.adam.step_count
+        self.adam = Adam(self._tensors, betas=self.adam.betas, eps=self.adam.eps)
+        self.adam.step_count = step_count
+        if exp_avg is not None:
+            for i, (a, b) in enumerate(zip(exp_avg, exp_avg_sq)):
+                self.adam.exp_avg[i].copy_(a.reshape(self._tensors[i].shape))
+                self.adam.exp_avg_sq[i].copy_(b.reshape(self._tensors[i].shape))
+
     def learning_rates(self, iteration):
         o = self.opt
         mu_lr = expon_lr(iteration, o.position_lr_init * self.spatial_lr_scale,

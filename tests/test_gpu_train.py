@@ -177,3 +177,30 @@ def test_train_step_checkpoint_resume(tmp_path):
     torch.cuda.synchronize()
     for p, q in zip(model.parameters(), fresh.parameters()):
         assert _rel(q, p) <= 1e-6
+
+
+def test_train_step_with_mcmc_density_control():
+    """relocate_gs + add_new_gs (nlosgr.densify) between fused steps: dead Gaussians revived, the
+    model grows by 5 %, Adam moments follow (zero for new / resampled entries) and training goes on."""
+    from nlosgr.densify import add_new_gs, prune_dead_mask, relocate_gs
+    from nlosgr.train import TrainStep
+    dev = torch.device("cuda:0")
+    torch.manual_seed(0)
+    scene, model, geo, cfg, target = _scene_model(dev)
+    step = TrainStep(model, geo, cfg, target, gt_times=100.0)
+    step()
+    model._opacity.data[:10] = -12.0
+    dead = prune_dead_mask(model)
+    assert int(dead.sum()) >= 10
+    relocate_gs(model, dead, train_step=step)
+    assert int(prune_dead_mask(model).sum()) == 0
+    ng0 = model._mu.shape[0]
+    added = add_new_gs(model, cap_max=10 * ng0, train_step=step)
+    assert added == int(1.05 * ng0) - ng0 and model._mu.shape[0] == ng0 + added
+    assert step.adam.exp_avg[0].shape[0] == ng0 + added
+    assert float(step.adam.exp_avg[0][ng0:].abs().sum()) == 0.0
+    loss2 = step()
+    torch.cuda.synchronize()
+    assert torch.isfinite(loss2).all()
+    for p in model.parameters():
+        assert torch.isfinite(p).all() and p.shape[0] == ng0 + added
