@@ -26,6 +26,7 @@
 //             registers; per-pair sums in LDS; per-Gaussian accumulators stay in registers
 //             for the whole split and are combined in a fixed order into a partial slab.
 #include <hip/hip_runtime.h>
+#include <type_traits>
 #include <math.h>
 #include <stdio.h>
 #include <string.h>
@@ -94,6 +95,9 @@ using namespace nlosgr::detail;
 #endif
 #ifndef NLOSGR_FVEC
 #define NLOSGR_FVEC 2          // vector drain width: float2 (2) or float4 (4) read-add-write (C3 fwd 248 vs 282 ms)
+#endif
+#ifndef NLOSGR_FHALF
+#define NLOSGR_FHALF 0         // forward vector drain: half rounds when most winners are in their tails (slower: 233 vs 230 ms)
 #endif
 #ifndef NLOSGR_BREC
 #define NLOSGR_BREC 1          // backward no-occlusion drain: exp2 recurrence + per-round moment sums
@@ -635,46 +639,63 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_F
             float t = d.t;
             float logT = d.logT;
             float xlo = d.xlo, elo = d.elo;
+            int nsr = kSteps;   // bins this round (the vector drain may run a half round, below)
             if (QUAD) {
-                // 16 bins from the quad holding pos: one ds_read_b128 + ds_write_b128 per 4 bins (the
-                // b32 read-add-write is bank-conflict bound).  Slots before pos (first round of a
-                // segment only) add 0 and do not advance the recurrence, which starts at pos.
+                // kSteps bins from the even (VW-aligned) bin at or below pos: one ds_read_b64 +
+                // ds_write_b64 per 2 bins.  Slots before pos (first round of a segment only) add 0 and
+                // do not advance the recurrence, which starts at pos.
                 const int o = d.pos & (VW - 1);
                 const int lim = remw + o;   // slot j is in the segment iff o <= j < lim
                 float cur = fast_exp2(fmaf(d.ga, t * t, d.al));
                 float q = fast_exp2(d.ga * fmaf(2.f, t, 1.f));
                 const float cc = fast_exp2(2.f * d.ga);
+                auto round_of = [&](auto ns_c) {
+                    constexpr int NS = decltype(ns_c)::value;
 #pragma unroll
-                for (int kv = 0; kv < kSteps / VW; ++kv) {
-                    float v[VW];
+                    for (int kv = 0; kv < NS / VW; ++kv) {
+                        float v[VW];
 #pragma unroll
-                    for (int jj = 0; jj < VW; ++jj) {
-                        const int j = VW * kv + jj;
-                        if (kv == 0) {
-                            const bool st = jj >= o;
-                            v[jj] = (st && j < lim) ? cur : 0.f;
-                            cur = st ? cur * q : cur;
-                            q = st ? q * cc : q;
-                        } else {
-                            v[jj] = j < lim ? cur : 0.f;
-                            cur *= q;
-                            q *= cc;
+                        for (int jj = 0; jj < VW; ++jj) {
+                            const int j = VW * kv + jj;
+                            if (kv == 0) {
+                                const bool st = jj >= o;
+                                v[jj] = (st && j < lim) ? cur : 0.f;
+                                cur = st ? cur * q : cur;
+                                q = st ? q * cc : q;
+                            } else {
+                                v[jj] = j < lim ? cur : 0.f;
+                                cur *= q;
+                                q *= cc;
+                            }
                         }
+                        if (VW == 4) {
+                            float4* hb4 = reinterpret_cast<float4*>(hb);
+                            float4 x = hb4[kv];
+                            x.x += v[0]; x.y += v[1]; x.z += v[2]; x.w += v[VW - 1];
+                            hb4[kv] = x;
+                        } else {
+                            float2* hb2 = reinterpret_cast<float2*>(hb);
+                            float2 x = hb2[kv];
+                            x.x += v[0]; x.y += v[VW - 1];
+                            hb2[kv] = x;
+                        }
+                        compiler_fence();
                     }
-                    if (VW == 4) {
-                        float4* hb4 = reinterpret_cast<float4*>(hb);
-                        float4 x = hb4[kv];
-                        x.x += v[0]; x.y += v[1]; x.z += v[2]; x.w += v[VW - 1];
-                        hb4[kv] = x;
-                    } else {
-                        float2* hb2 = reinterpret_cast<float2*>(hb);
-                        float2 x = hb2[kv];
-                        x.x += v[0]; x.y += v[VW - 1];
-                        hb2[kv] = x;
-                    }
-                    compiler_fence();
+                };
+                // half round when most winners would leave most of a full round empty (segment tails)
+                bool half = false;
+                if (NLOSGR_FHALF) {
+                    const int nwin = __popcll(__builtin_amdgcn_ballot_w64(win));
+                    const int nshort = __popcll(__builtin_amdgcn_ballot_w64(win && lim <= kSteps / 2));
+                    half = 2 * nshort > nwin;
                 }
-                t += (float)(kSteps - o);
+                if (half) {
+                    round_of(std::integral_constant<int, kSteps / 2>());
+                    nsr = kSteps / 2;
+                } else {
+                    round_of(std::integral_constant<int, kSteps>());
+                }
+                t += (float)(nsr - o);
             } else if (NLOSGR_FREC && MODE == NLOSGR_MODE_NOOCL && !RAYS && !DENSE) {
                 // value(t+1) = value(t) q(t), q(t+1) = q(t) 2^(2 ga): two multiplies per bin instead of
                 // mul + fma + exp2; seeded with exact exp2 every round (see kRecurrence)
@@ -749,7 +770,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_F
                 compiler_fence();
             }
             if (win) {
-                const int adv = QUAD ? kSteps - (d.pos & (NLOSGR_FVEC - 1)) : kSteps;
+                const int adv = QUAD ? nsr - (d.pos & (NLOSGR_FVEC - 1)) : kSteps;
                 d.t = t;
                 d.logT = logT;
                 d.xlo = xlo;
