@@ -100,6 +100,12 @@ def main():
     ap.add_argument("--cutoff", type=float, default=3.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-json", default="")
+    ap.add_argument("--band", type=int, default=0,
+                    help="render only wall band 0 of BAND equal bands (one rank's share of a BAND-GPU sharded "
+                         "volume, nlosgr.distributed.wall_band); value = projected volumes/s of the sharded job")
+    ap.add_argument("--shard", action="store_true",
+                    help="with N ranks, rank r renders wall band r of N (SURVEY §8e: one volume per step over "
+                         "the whole job, packed gradient all-reduce timed) -> strong scaling")
     a = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -119,17 +125,27 @@ def main():
     ng, H, W, T, ns, fwd_only = CONFIGS[a.config]
     scene = Scene(H=H, W=W, T=T, ns=ns)
     model = GaussianParams.synthetic(ng, 3, preset="cuda", device=dev, seed=0)
-    geo = scene.geometry(dev, "cuda", "noocl")
+    nwall = H * W
+    if a.shard and world > 1 and a.band > 1:
+        raise SystemExit("--band is a single-GPU projection; with N ranks use --shard")
+    band_n, band_r = (world, rank) if (a.shard and world > 1) else (a.band, 0)
+    if band_n > 1:   # one rank's contiguous band of the wall (SURVEY §8e sharding)
+        from nlosgr.distributed import wall_band
+        b0, b1 = wall_band(H * W, band_r, band_n)
+        geo = scene.geometry(dev, "cuda", "noocl", walls=scene.walls(dev)[b0:b1].contiguous())
+        nwall = b1 - b0
+    else:
+        geo = scene.geometry(dev, "cuda", "noocl")
     cfg = make_config(model, scene, "cuda", "noocl", cutoff=a.cutoff)
     g = torch.Generator().manual_seed(1 + rank)
-    target = (torch.rand(H * W, T, generator=g) * 1e-3).to(dev)   # measured volume, x gt_times=100 in the loss
+    target = (torch.rand(nwall, T, generator=g) * 1e-3).to(dev)   # measured volume, x gt_times=100 in the loss
     ev_fwd = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     ev_bwd = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     fwd_ms, bwd_ms = [], []
     # one training iteration of the reference (main.py:198-214) over the whole volume, fused on the
     # device: forward (records the ray cache) -> MSE vs gt_times * target + dL/dhist -> backward
     # (walks the ray cache) -> [packed gradient all-reduce] -> Adam over the six parameter groups
-    train = TrainStep(model, geo, cfg, target, gt_times=100.0, nwall_total=H * W * world,
+    train = TrainStep(model, geo, cfg, target, gt_times=100.0, nwall_total=H * W if band_n > 1 else H * W * world,
                       events={"fwd": ev_fwd, "bwd": ev_bwd})
     stream = torch.cuda.current_stream(dev)
 
@@ -166,11 +182,12 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
     ms_per_step = elapsed * 1000.0 / a.steps
-    volumes_per_s = world * a.steps / elapsed
+    # weak (replicas): every rank finishes one volume per step; sharded: the job finishes one
+    volumes_per_s = (1 if a.shard and world > 1 else world) * a.steps / elapsed
 
     # roofline of the dominant phase (algorithmic HBM bytes / measured launch time)
     pb = param_bytes(3)
-    V = 4 * H * W * T
+    V = 4 * nwall * T
     fwd_avg = sum(fwd_ms) / len(fwd_ms)
     bwd_avg = sum(bwd_ms) / len(bwd_ms) if bwd_ms else 0.0
     if bwd_avg >= fwd_avg:
@@ -195,13 +212,17 @@ def main():
         "metric": "transient volumes/sec (fwd+bwd), 100k Gaussians → 128×128×1024 ToF bins"
         if a.config == "C3" else f"transient volumes/sec ({'fwd' if fwd_only else 'fwd+bwd'}) {a.config}",
         "value": volumes_per_s, "unit": "volumes/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
-        "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "strong" if a.shard and world > 1 else "weak", "vs_baseline": None,
         "dtype": "f32", "data": "synthetic (SURVEY §8d geometry, seeded random Gaussians and target)",
         "config": {"workload": f"{a.config}: {ng} Gaussians -> {H}x{W} wall x {T} bins, {ns}x{ns} angular "
                                f"samples, cuda preset, no occlusion, support cutoff {a.cutoff} sigma, "
                                f"{'fwd' if fwd_only else 'fwd+MSE+bwd (6 param grads)+Adam'}",
                    "gaussians": ng, "wall": [H, W], "bins": T, "angular": ns, "cutoff": a.cutoff,
-                   "parallelism": f"wall-replica x{world}, grad all-reduce" if world > 1 else "single GPU"},
+                   "parallelism": (f"wall shard: {world} bands (rank r renders band r), packed grad "
+                                   f"all-reduce" if a.shard and world > 1 else
+                                   f"one rank's band of a {a.band}-way wall shard (projected job rate; the "
+                                   f"packed gradient all-reduce is not timed)" if a.band > 1 else
+                                   f"wall-replica x{world}, grad all-reduce" if world > 1 else "single GPU")},
         "phase_ms": {"fwd": fwd_avg, "bwd": bwd_avg},
         "roofline": {"bound": "hbm", "kernel": f"nlosgr {dom} ({' + '.join(kern)})", "achieved": achieved,
                      "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS,

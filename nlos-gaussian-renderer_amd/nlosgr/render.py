@@ -16,7 +16,7 @@ import torch
 from . import _lib
 
 # upper bound on the forward->backward ray cache (24 B per wall point x Gaussian pair; C3: 39 GB)
-RAY_CACHE_MAX_BYTES = int(float(os.environ.get("NLOSGR_RAY_CACHE_GB", "96")) * 2 ** 30)
+RAY_CACHE_MAX_BYTES = int(float(os.environ.get("NLOSGR_RAY_CACHE_GB", "128")) * 2 ** 30)   # of 288 GB HBM
 
 
 @dataclass(frozen=True)
