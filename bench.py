@@ -111,10 +111,13 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # NLOSGR_DIST_BACKEND=gloo rehearses N ranks on fewer GPUs (rank -> GPU local % count); the
+    # production path is RCCL ("nccl"), one GPU per rank
+    ndev = max(1, torch.cuda.device_count())
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
-    dev = torch.device("cuda", local)
+        torch.cuda.set_device(local % ndev)
+        dist.init_process_group(os.environ.get("NLOSGR_DIST_BACKEND", "nccl"))
+    dev = torch.device("cuda", local % ndev)
 
     from nlosgr import GaussianParams
     from nlosgr.model import features_flat

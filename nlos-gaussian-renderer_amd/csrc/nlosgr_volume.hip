@@ -99,6 +99,9 @@ using namespace nlosgr::detail;
 #ifndef NLOSGR_FHALF
 #define NLOSGR_FHALF 0         // forward vector drain: half rounds when most winners are in their tails (slower: 233 vs 230 ms)
 #endif
+#ifndef NLOSGR_TIGHT_BOX
+#define NLOSGR_TIGHT_BOX 1     // (theta, phi) candidate box = samples inside the cap range (0: one extra sample per side)
+#endif
 #ifndef NLOSGR_BREC
 #define NLOSGR_BREC 1          // backward no-occlusion drain: exp2 recurrence + per-round moment sums
 #endif
@@ -223,8 +226,10 @@ __device__ __forceinline__ void pair_setup(const KArgs& k, const float* f, const
     const float th0 = lin[0], dth = lin[1], ph0 = lin[2], dph = lin[3];
     if (dth > 0.f) {
         const float idth = frcp(dth);
-        P.i0 = fidx(floorf((thc - alpha - th0) * idth), 0, nt - 1);
-        P.i1 = fidx(ceilf((thc + alpha - th0) * idth), -1, nt - 1);
+        // samples are points (theta_i = th0 + i dth): the box holds exactly the samples inside the
+        // margin-widened cap range, [ceil(lo), floor(hi)] (floor/ceil added one outside row per side)
+        P.i0 = fidx(NLOSGR_TIGHT_BOX ? ceilf((thc - alpha - th0) * idth) : floorf((thc - alpha - th0) * idth), 0, nt - 1);
+        P.i1 = fidx(NLOSGR_TIGHT_BOX ? floorf((thc + alpha - th0) * idth) : ceilf((thc + alpha - th0) * idth), -1, nt - 1);
     }
     if (thc - alpha > 1e-3f && thc + alpha < kPi - 1e-3f && dph > 0.f) {
         // max |phi - phi_c| on the cone = asin(sin(alpha) / sin(theta_c))
@@ -237,8 +242,8 @@ __device__ __forceinline__ void pair_setup(const KArgs& k, const float* f, const
             const float lo = phc - dphi, hi = phc + dphi;
             if (lo > -kPi && hi < kPi) {
                 const float idph = frcp(dph);
-                P.j0 = fidx(floorf((lo - ph0) * idph), 0, np_ - 1);
-                P.j1 = fidx(ceilf((hi - ph0) * idph), -1, np_ - 1);
+                P.j0 = fidx(NLOSGR_TIGHT_BOX ? ceilf((lo - ph0) * idph) : floorf((lo - ph0) * idph), 0, np_ - 1);
+                P.j1 = fidx(NLOSGR_TIGHT_BOX ? floorf((hi - ph0) * idph) : ceilf((hi - ph0) * idph), -1, np_ - 1);
             }
         }
     }
