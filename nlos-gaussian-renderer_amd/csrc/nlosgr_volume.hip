@@ -30,6 +30,7 @@
 #include <math.h>
 #include <stdio.h>
 #include <string.h>
+#include <stdlib.h>
 
 #include "nlosgr_common.hpp"
 
@@ -129,6 +130,7 @@ struct KArgs {
     float* shpart;               // sh_kernel partials [nsh][ng][kShPart]
     int nsh;                     // sh_kernel wall-point splits
     int nfsplit;                 // forward Gaussian splits per wall point (hpart != null)
+    int bshared;                 // backward: 4 waves share each wall point's staged row (bwd_shared)
     unsigned* cbox;              // ray cache [P][ng]: i0 | j0 << 12 | width << 24, 0 = not cached
     float* crho;                 // ray cache [P][ng]: the pair's SH albedo rho (NLOSGR_BRHO)
 };
@@ -850,9 +852,30 @@ constexpr int kBSteps = NLOSGR_BSTEPS;   // bins per lane per backward drain rou
 constexpr int kBwdSlots = 13;   // per-Gaussian backward partial: dA[9], dMu[3], dsigma (stride 32 in HBM)
 constexpr int kShPart = 20;     // sh_kernel partial: dF[16], dMu[3], pad
 
+// Two layouts.  Per-wave rows (default): each wave walks its own wall points and stages its own
+// upstream-gradient row and angle tables.  Shared rows (bwd_shared, long rows): the workgroup's 4
+// waves own 4 x 64 Gaussians and walk the same wall points; one double-buffered row + tables per
+// workgroup (staged by all 256 threads one wall point ahead, one barrier per wall point), so the
+// LDS no longer scales with 4 x nr (C5, nr = 2048: 56 KB -> 39 KB per workgroup, 2 -> 4 per CU).
 struct BwdLayout {
-    int wave_base, wave_stride, grow, tth, tph, rayq, owner, owner2, pdat, red, total;
-    __host__ __device__ BwdLayout(int nr, int nt, int np_) {
+    int wave_base, wave_stride, grow, tth, tph, rayq, owner, owner2, pdat, red, total, buf_stride;
+    __host__ __device__ BwdLayout(int nr, int nt, int np_, bool shared = false) {
+        buf_stride = 0;
+        if (shared) {
+            grow = 0;                                 // buffer b at smem + b * buf_stride
+            tth = al4(nr + kBSteps);
+            tph = tth + al4(2 * nt);
+            buf_stride = tph + al4(2 * np_);
+            wave_base = 2 * buf_stride;
+            rayq = 0;                                 // per-wave region (relative to the wave's base)
+            owner = rayq + kRQ;
+            owner2 = owner + 64;
+            pdat = owner2 + (NLOSGR_BDUAL ? 64 : 0);
+            wave_stride = al4(pdat + 64 * 16);
+            red = 0;                                  // unused: waves own distinct Gaussians
+            total = wave_base + kWaves * wave_stride;
+            return;
+        }
         wave_base = 0;
         grow = 0;                            // [nr + kBSteps] upstream gradient x att x hscale, zero pad
         tth = al4(nr + kBSteps);             // float2 [nt]
@@ -916,6 +939,32 @@ __device__ __forceinline__ void stage_grow(const float* grad, const float* att, 
         for (int t = lane; t < nr; t += 64) grow[t] = grad ? grad[t] * att[t] * hs : 0.f;
     }
     for (int t = nr + lane; t < nr + kBSteps; t += 64) grow[t] = 0.f;
+}
+
+// shared layout: the whole workgroup stages wall point p's row and tables into one buffer
+__device__ __forceinline__ void stage_shared(const KArgs& k, int p, int nr, int nt, int np_, float* grow, float2* tth,
+                                             float2* tph) {
+    const int t0 = threadIdx.x;
+    const float hs = k.geo.hscale[p];
+    const float* grad = k.grad_hist ? k.grad_hist + (size_t)p * nr : nullptr;
+    const float* att = k.geo.att;
+    if (grad && (nr & 3) == 0 && ((reinterpret_cast<uintptr_t>(grad) | reinterpret_cast<uintptr_t>(att)) & 15) == 0) {
+        const float4* g4 = reinterpret_cast<const float4*>(grad);
+        const float4* a4 = reinterpret_cast<const float4*>(att);
+        const int n4 = nr >> 2;
+        for (int t = t0; t < n4; t += kBlock) {
+            const float4 gv = g4[t], av = a4[t];
+            reinterpret_cast<float4*>(grow)[t] =
+                make_float4(gv.x * av.x * hs, gv.y * av.y * hs, gv.z * av.z * hs, gv.w * av.w * hs);
+        }
+    } else {
+        for (int t = t0; t < nr; t += kBlock) grow[t] = grad ? grad[t] * att[t] * hs : 0.f;
+    }
+    for (int t = nr + t0; t < nr + kBSteps; t += kBlock) grow[t] = 0.f;
+    for (int t = t0; t < nt; t += kBlock)
+        tth[t] = make_float2(k.geo.sin_theta[(size_t)p * nt + t], k.geo.cos_theta[(size_t)p * nt + t]);
+    for (int t = t0; t < np_; t += kBlock)
+        tph[t] = make_float2(k.geo.cos_phi[(size_t)p * np_ + t], k.geo.sin_phi[(size_t)p * np_ + t]);
 }
 
 // register prefetch of one wall point's backward inputs (see bwd_kernel)
@@ -983,23 +1032,25 @@ __device__ __forceinline__ bool bray_setup(const float* pd, float2 th, float2 ph
     return true;
 }
 
-template <int PRESET, int MODE, bool DENSE, bool RAYS, bool CACHE>
+template <int PRESET, int MODE, bool DENSE, bool RAYS, bool CACHE, bool SHR>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_BWD_WAVES, 8))) void bwd_kernel(KArgs k) {
     extern __shared__ __align__(16) float smem[];
     const int nr = k.geo.nr, nt = k.geo.nt, np_ = k.geo.np, P_ = k.geo.nwall;
-    const BwdLayout L(nr, nt, np_);
+    constexpr bool shr = SHR;   // == (k.bshared != 0)
+    const BwdLayout L(nr, nt, np_, shr);
     const int wave = threadIdx.x >> 6, lane = lane_id();
     float* wb = smem + L.wave_base + wave * L.wave_stride;
-    float* grow = wb + L.grow;
-    float2* tth = reinterpret_cast<float2*>(wb + L.tth);
-    float2* tph = reinterpret_cast<float2*>(wb + L.tph);
+    float* gbase = shr ? smem : wb;
+    float* grow = gbase + L.grow;
+    float2* tth = reinterpret_cast<float2*>(gbase + L.tth);
+    float2* tph = reinterpret_cast<float2*>(gbase + L.tph);
     unsigned* rayq = reinterpret_cast<unsigned*>(wb + L.rayq);
     unsigned* owner = reinterpret_cast<unsigned*>(wb + L.owner);
     unsigned* owner2 = reinterpret_cast<unsigned*>(wb + L.owner2);
     float* pdat = wb + L.pdat;
 
-    const int gb = blockIdx.x * kNB;
-    const int gi = gb + lane;
+    const int gb = blockIdx.x * (shr ? kNB * kWaves : kNB);
+    const int gi = gb + (shr ? wave * kNB : 0) + lane;
     const bool active = gi < k.g.ng;
     const int split = blockIdx.y;
     const int per = (P_ + k.nsplit - 1) / k.nsplit;
@@ -1030,18 +1081,31 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_B
     // software pipeline over wall points: the next wall point's upstream gradient row and
     // angle tables are loaded into registers while this one is processed (common shapes:
     // nr <= 1024, nr % 4 == 0, nt, np <= 64); other shapes stage synchronously
-    const bool pf = NLOSGR_BWD_PF && k.grad_hist && nr <= 4 * 64 * kPFRow && (nr & 3) == 0 && nt <= 64 && np_ <= 64 &&
+    const bool pf = NLOSGR_BWD_PF && !shr && k.grad_hist && nr <= 4 * 64 * kPFRow && (nr & 3) == 0 && nt <= 64 && np_ <= 64 &&
                     ((reinterpret_cast<uintptr_t>(k.grad_hist) | reinterpret_cast<uintptr_t>(k.geo.att)) & 15) == 0;
     RowPF rpf;
     if (pf && pbeg + wave < pend) rpf.load(k, pbeg + wave, nr, nt, np_);
-    const bool glds = NLOSGR_BGLDS && k.growall != nullptr;   // host guarantees nr % 256 == 0
+    const bool glds = NLOSGR_BGLDS && !shr && k.growall != nullptr;   // host guarantees nr % 256 == 0
     if (glds)
         for (int t = nr + lane; t < nr + kBSteps; t += 64) grow[t] = 0.f;   // pad: never overwritten
-    for (int p = pbeg + wave; p < pend; p += kWaves) {
-        // stage this wall point's upstream gradient row and tables (wave-private)
+    if (shr && pbeg < pend) stage_shared(k, pbeg, nr, nt, np_, grow, tth, tph);
+    int it = 0;
+    for (int p = pbeg + (shr ? 0 : wave); p < pend; p += (shr ? 1 : kWaves), ++it) {
+        // stage this wall point's upstream gradient row and tables (wave-private), or (shared) make
+        // the buffer staged one wall point ahead current and stage the next one into the other
         const float hs = k.geo.hscale[p];
         wave_sync();
-        if (glds) {
+        if (shr) {
+            __syncthreads();   // buffer it & 1 complete; every wave is done with wall point p - 1
+            float* bnext = smem + ((it + 1) & 1) * L.buf_stride;
+            if (p + 1 < pend)
+                stage_shared(k, p + 1, nr, nt, np_, bnext + L.grow, reinterpret_cast<float2*>(bnext + L.tth),
+                             reinterpret_cast<float2*>(bnext + L.tph));
+            float* bcur = smem + (it & 1) * L.buf_stride;
+            grow = bcur + L.grow;
+            tth = reinterpret_cast<float2*>(bcur + L.tth);
+            tph = reinterpret_cast<float2*>(bcur + L.tph);
+        } else if (glds) {
             // 1 KiB per wave-instruction straight into LDS; retired before the drain (s_waitcnt below)
             const float* row = k.growall + (size_t)p * nr;
             for (int c = 0; c < nr; c += 256)
@@ -1431,6 +1495,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_B
     }
     if (NLOSGR_DIAG && (k.opt.flags & 8) && k.counts && lane == 0)
         for (int c = 0; c < 5; ++c) atomicAdd(k.counts + c, dg[c]);
+    if (shr) {   // shared layout: every wave owns its Gaussians for the whole split
+        if (active) {
+            float* dst = k.partial + ((size_t)split * k.g.ng + gi) * 32;
+            for (int t = 0; t < 9; ++t) dst[t] = dA[t];
+            dst[9] = dMu[0]; dst[10] = dMu[1]; dst[11] = dMu[2];
+            dst[12] = dSig;
+        }
+        return;
+    }
     // fixed-order combination of the 4 waves' accumulators -> partial slab
     __syncthreads();
     float* red = smem + L.red;
@@ -1575,6 +1648,8 @@ __global__ __launch_bounds__(kBlock) void bbox_kernel(nlosgr_gaussians g, float 
 // host side
 // ------------------------------------------------------------------------------------------
 
+bool bwd_shared(const nlosgr_geometry* geo);
+
 int validate(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_options* opt) {
     if (!g || !geo || !opt) return set_err(NLOSGR_E_INVALID, "null argument struct");
     if (g->ng < 0) return set_err(NLOSGR_E_INVALID, "ng must be >= 0");
@@ -1596,21 +1671,37 @@ int validate(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr
                            !geo->cos_phi || !geo->grid_lin || !geo->hscale || !geo->r || !geo->att))
         return set_err(NLOSGR_E_INVALID, "null geometry pointer");
     const size_t lds_f = (size_t)FwdLayout(geo->nr, geo->nt, geo->np).total * 4;
-    const size_t lds_b = (size_t)BwdLayout(geo->nr, geo->nt, geo->np).total * 4;
+    const size_t lds_b = (size_t)BwdLayout(geo->nr, geo->nt, geo->np, bwd_shared(geo)).total * 4;
     if (lds_f > 160 * 1024 || lds_b > 160 * 1024) return set_err(NLOSGR_E_UNSUPPORTED, "problem exceeds LDS budget");
     return NLOSGR_OK;
 }
 
-int bwd_nsplit(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_options* opt) {
+// shared-row backward layout when per-wave rows would leave fewer than 4 workgroups per CU
+// (long rows, e.g. C5's 2048 bins); NLOSGR_BSHARED=0/1 forces either layout (A/B timing)
+bool bwd_shared(const nlosgr_geometry* geo) {
+    const char* e = getenv("NLOSGR_BSHARED");
+    if (e && (e[0] == '0' || e[0] == '1')) return e[0] == '1';
+    return (size_t)BwdLayout(geo->nr, geo->nt, geo->np).total * 4 > 40 * 1024;
+}
+
+int bwd_nsplit(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_options* opt, bool shared) {
     const int maxs = geo->nwall > 0 ? geo->nwall : 1;
     if (opt->nsplit > 0) return opt->nsplit < maxs ? opt->nsplit : maxs;
-    const int nblk = (g->ng + kNB - 1) / kNB;
+    const int gpb = shared ? kNB * kWaves : kNB;
+    const int nblk = (g->ng + gpb - 1) / gpb;
     // aim for ~48k workgroups: with 4 resident per CU a 3k-workgroup grid left a long last round
     // (C3 backward: 2 splits 354 ms, 16 -> 309, 32 -> 305, 64 -> 302)
     int ns = (49152 + nblk - 1) / (nblk > 0 ? nblk : 1);
     if (ns > maxs) ns = maxs;
     if (ns < 1) ns = 1;
     return ns;
+}
+
+// partial-slab splits the workspace layout reserves: the larger of the two layouts, so the ray
+// cache's offset does not depend on which layout a later backward picks (NLOSGR_BSHARED)
+int bwd_nsplit_ws(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_options* opt) {
+    const int a = bwd_nsplit(g, geo, opt, false), b = bwd_nsplit(g, geo, opt, true);
+    return a > b ? a : b;
 }
 
 
@@ -1621,8 +1712,12 @@ void launch_fwd(const KArgs& ka, size_t shm, hipStream_t s) {
 }
 template <int PRESET, int MODE, bool DENSE, bool RAYS, bool CACHE>
 void launch_bwd(const KArgs& ka, size_t shm, hipStream_t s) {
-    dim3 grid((ka.g.ng + kNB - 1) / kNB, ka.nsplit);
-    hipLaunchKernelGGL((bwd_kernel<PRESET, MODE, DENSE, RAYS, CACHE>), grid, dim3(kBlock), shm, s, ka);
+    const int gpb = ka.bshared ? kNB * kWaves : kNB;
+    dim3 grid((ka.g.ng + gpb - 1) / gpb, ka.nsplit);
+    if (ka.bshared)
+        hipLaunchKernelGGL((bwd_kernel<PRESET, MODE, DENSE, RAYS, CACHE, true>), grid, dim3(kBlock), shm, s, ka);
+    else
+        hipLaunchKernelGGL((bwd_kernel<PRESET, MODE, DENSE, RAYS, CACHE, false>), grid, dim3(kBlock), shm, s, ka);
 }
 
 // the ray cache is used only by the culled, histogram-only variants (the training hot path)
@@ -1704,11 +1799,11 @@ int run_fwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_
     ka.recs = (const GaussRec*)workspace;
     ka.hist_out = hist_out; ka.ray_out = ray_out;
     ka.counts = counts;
-    if (!counts) cache_ptrs(g, geo, opt, workspace, bwd_nsplit(g, geo, opt), ka);
+    if (!counts) cache_ptrs(g, geo, opt, workspace, bwd_nsplit_ws(g, geo, opt), ka);
     const int nfs = fwd_nsplit(g, geo);
     if (hist_out && nfs > 1 && g->ng > 0) {
         ka.hpart = (float*)((char*)workspace + align_up((size_t)g->ng * sizeof(GaussRec)) +
-                            align_up((size_t)bwd_nsplit(g, geo, opt) * g->ng * 32 * sizeof(float)) +
+                            align_up((size_t)bwd_nsplit_ws(g, geo, opt) * g->ng * 32 * sizeof(float)) +
                             cache_bytes(g, geo, opt) + sh_bytes(g, geo) + 256);
         ka.nfsplit = nfs;
     }
@@ -1749,7 +1844,7 @@ const char* nlosgr_last_error(void) { return g_err; }
 size_t nlosgr_workspace_bytes(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_options* opt) {
     if (validate(g, geo, opt) != NLOSGR_OK) return 0;
     const size_t rec = align_up((size_t)g->ng * sizeof(GaussRec));
-    const size_t part = align_up((size_t)bwd_nsplit(g, geo, opt) * g->ng * 32 * sizeof(float));
+    const size_t part = align_up((size_t)bwd_nsplit_ws(g, geo, opt) * g->ng * 32 * sizeof(float));
     return rec + part + cache_bytes(g, geo, opt) + sh_bytes(g, geo) + 256 + fpart_bytes(g, geo) +
            (NLOSGR_BGLDS ? align_up((size_t)geo->nwall * geo->nr * sizeof(float)) : 0);   // grow_kernel rows
 }
@@ -1792,11 +1887,12 @@ int nlosgr_render_bwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo, con
     ka.recs = (const GaussRec*)workspace;
     ka.partial = (float*)((char*)workspace + align_up((size_t)g->ng * sizeof(GaussRec)));
     ka.grad_hist = grad_hist; ka.grad_ray = grad_ray;
-    ka.nsplit = bwd_nsplit(g, geo, opt);
-    cache_ptrs(g, geo, opt, workspace, ka.nsplit, ka);
+    ka.bshared = bwd_shared(geo) ? 1 : 0;
+    ka.nsplit = bwd_nsplit(g, geo, opt, ka.bshared != 0);
+    cache_ptrs(g, geo, opt, workspace, bwd_nsplit_ws(g, geo, opt), ka);
     {
         char* shb = (char*)workspace + align_up((size_t)g->ng * sizeof(GaussRec)) +
-                    align_up((size_t)ka.nsplit * g->ng * 32 * sizeof(float)) + cache_bytes(g, geo, opt);
+                    align_up((size_t)bwd_nsplit_ws(g, geo, opt) * g->ng * 32 * sizeof(float)) + cache_bytes(g, geo, opt);
         ka.drho = (float*)shb;
         ka.shpart = (float*)(shb + align_up((size_t)geo->nwall * g->ng * sizeof(float)));
         ka.nsh = sh_nsplit(g, geo);
@@ -1816,7 +1912,7 @@ int nlosgr_render_bwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo, con
     launch_preprocess(g, (GaussRec*)workspace, s);
     HIPCHK(hipGetLastError());
     if (geo->nwall > 0 && (grad_hist || grad_ray)) {
-        const size_t shm = (size_t)BwdLayout(geo->nr, geo->nt, geo->np).total * sizeof(float);
+        const size_t shm = (size_t)BwdLayout(geo->nr, geo->nt, geo->np, ka.bshared != 0).total * sizeof(float);
         const bool dense = !(opt->cutoff > 0.f);
         const bool rays = grad_ray != nullptr;
         if (g->preset == NLOSGR_PRESET_TORCH) {

@@ -198,3 +198,39 @@ def test_ray_cache_backward_matches_uncached(mode):
     got = render_backward(*args, cfg, grad_hist=g, workspace=ws, ray_cache=True)
     for name, a, b in zip(["mu", "scaling", "rotation", "opacity", "features"], got, ref):
         _close(a.cpu(), b.cpu(), 1e-5, 1e-9, f"cached grad {name}")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["noocl", "netf"])
+def test_bwd_shared_layout_matches_per_wave(mode, monkeypatch):
+    """The shared-row backward layout (4 waves own 256 Gaussians and share each wall point's
+    staged row; chosen automatically for long rows, NLOSGR_BSHARED forces it) gives the per-wave
+    layout's gradients within fp32 summation-order noise, with and without the ray cache, for a
+    ragged Gaussian count and a workspace allocated under the other layout."""
+    from nlosgr import GaussianParams, features_flat
+    from nlosgr.volume import Scene, make_config
+    from nlosgr.render import render_backward, render_forward
+    dev = torch.device("cuda:0")
+    scene = Scene(H=5, W=7, T=512, ns=16)
+    m = GaussianParams.synthetic(1999, 3, preset="cuda", device=dev, seed=6)
+    geo = scene.geometry(dev, "cuda", mode)
+    cfg = make_config(m, scene, mode=mode, cutoff=3.0)
+    args = (m._mu.detach(), m._scaling.detach(), m._rotation.detach(), m._opacity.detach(),
+            features_flat(m).detach().contiguous(), geo)
+    g = torch.randn((scene.H * scene.W, scene.T), generator=torch.Generator().manual_seed(8)).to(dev) * 1e-3
+    monkeypatch.setenv("NLOSGR_BSHARED", "0")
+    h0, _, ws = render_forward(*args, cfg, ray_cache=True)
+    ref = render_backward(*args, cfg, grad_hist=g)
+    ref_c = render_backward(*args, cfg, grad_hist=g, workspace=ws, ray_cache=True)
+    monkeypatch.setenv("NLOSGR_BSHARED", "1")
+    got = render_backward(*args, cfg, grad_hist=g)
+    got_c = render_backward(*args, cfg, grad_hist=g, workspace=ws, ray_cache=True)   # ws from the other layout
+    h1, _, ws1 = render_forward(*args, cfg, ray_cache=True)
+    got_c1 = render_backward(*args, cfg, grad_hist=g, workspace=ws1, ray_cache=True)
+    assert torch.equal(h0, h1)
+    for name, a, b, c, d in zip(["mu", "scaling", "rotation", "opacity", "features"], got, ref, got_c, got_c1):
+        _close(a.cpu(), b.cpu(), 1e-5, 1e-9, f"shared grad {name}")
+        _close(c.cpu(), b.cpu(), 1e-5, 1e-9, f"shared cached grad {name}")
+        _close(d.cpu(), b.cpu(), 1e-5, 1e-9, f"shared cached (own ws) grad {name}")
+    for a, b in zip(ref_c, ref):
+        _close(a.cpu(), b.cpu(), 1e-5, 1e-9, "per-wave cached")
