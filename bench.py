@@ -40,8 +40,8 @@ def param_bytes(deg):
     return 4 * (3 + 3 + 4 + 1 + (deg + 1) ** 2)        # 108 B at SH degree 3
 
 
-def cpu_baseline(cfg_name, seed=0):
-    """Time the CPU oracle (dense restatement of the reference's torch path, cuda preset) on a
+def cpu_baseline(cfg_name, seed=0, preset="cuda", mode="noocl"):
+    """Time the CPU oracle (dense restatement of the reference path, same preset and mode as the GPU run) on a
     bounded sample of the same workload: 1 wall point x G_SAMPLE of the Ng Gaussians x the full
     Ns^2 x T sample grid, fwd+bwd, in chunks of 32 Gaussians (bounded memory); extrapolated
     linearly (the dense cost is linear in Gaussians and in wall points)."""
@@ -53,7 +53,7 @@ def cpu_baseline(cfg_name, seed=0):
     torch.set_num_threads(threads)
     scene = Scene(H=H, W=W, T=T, ns=ns)
     g_sample = max(1, min(ng, int(os.environ.get("NLOSGR_CPU_SAMPLE_G", "160"))))
-    m = GaussianParams.synthetic(ng, 3, preset="cuda", device="cpu", seed=seed)
+    m = GaussianParams.synthetic(ng, 3, preset=preset, device="cpu", seed=seed)
     walls = scene.walls("cpu")
     p = walls[(H // 2) * W + W // 2]
     tab = R.sample_tables(p, scene.box("cpu"), ns, scene.start, scene.end, scene.c, scene.deltaT)
@@ -62,12 +62,12 @@ def cpu_baseline(cfg_name, seed=0):
         sl = slice(g0, min(g_sample, g0 + 32))
         P = R.Params(*(t.detach()[sl].clone() for t in (m._mu, m._scaling, m._rotation, m._opacity,
                                                         m._features_dc, m._features_rest)), 3)
-        _, h = R.render_wallpoint(P, p, tab, 0.5, scene.c, scene.deltaT, preset="cuda", mode="noocl")
+        _, h = R.render_wallpoint(P, p, tab, 0.5, scene.c, scene.deltaT, preset=preset, mode=mode)
         (h * h).sum().backward()
     t = time.perf_counter() - t0
     per_volume = t * (ng / g_sample) * (H * W)
     return {"value": 1.0 / per_volume, "unit": "volumes/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/torch_ref dense (cuda preset) fwd+bwd of 1 wall point x {g_sample} of {ng} "
+            "sample": f"oracle/torch_ref dense ({preset} preset, {mode}) fwd+bwd of 1 wall point x {g_sample} of {ng} "
                       f"Gaussians x {ns}x{ns}x{T} samples = {t:.2f} s on {threads} threads; "
                       f"extrapolated x{ng / g_sample:g} Gaussians x{H * W} wall points"}
 
@@ -100,6 +100,10 @@ def main():
     ap.add_argument("--cutoff", type=float, default=3.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-json", default="")
+    ap.add_argument("--preset", default="cuda", choices=("cuda", "torch"),
+                    help="convention preset: cuda = the reference's CUDA path, torch = its torch path (SURVEY A.3)")
+    ap.add_argument("--mode", default="noocl", choices=("noocl", "netf"),
+                    help="rendering_type: noocl (configs/default.py:15 default) or netf self-transmittance")
     ap.add_argument("--band", type=int, default=0,
                     help="render only wall band 0 of BAND equal bands (one rank's share of a BAND-GPU sharded "
                          "volume, nlosgr.distributed.wall_band); value = projected volumes/s of the sharded job")
@@ -127,7 +131,7 @@ def main():
 
     ng, H, W, T, ns, fwd_only = CONFIGS[a.config]
     scene = Scene(H=H, W=W, T=T, ns=ns)
-    model = GaussianParams.synthetic(ng, 3, preset="cuda", device=dev, seed=0)
+    model = GaussianParams.synthetic(ng, 3, preset=a.preset, device=dev, seed=0)
     nwall = H * W
     if a.shard and world > 1 and a.band > 1:
         raise SystemExit("--band is a single-GPU projection; with N ranks use --shard")
@@ -135,11 +139,11 @@ def main():
     if band_n > 1:   # one rank's contiguous band of the wall (SURVEY §8e sharding)
         from nlosgr.distributed import wall_band
         b0, b1 = wall_band(H * W, band_r, band_n)
-        geo = scene.geometry(dev, "cuda", "noocl", walls=scene.walls(dev)[b0:b1].contiguous())
+        geo = scene.geometry(dev, a.preset, a.mode, walls=scene.walls(dev)[b0:b1].contiguous())
         nwall = b1 - b0
     else:
-        geo = scene.geometry(dev, "cuda", "noocl")
-    cfg = make_config(model, scene, "cuda", "noocl", cutoff=a.cutoff)
+        geo = scene.geometry(dev, a.preset, a.mode)
+    cfg = make_config(model, scene, a.preset, a.mode, cutoff=a.cutoff)
     g = torch.Generator().manual_seed(1 + rank)
     target = (torch.rand(nwall, T, generator=g) * 1e-3).to(dev)   # measured volume, x gt_times=100 in the loss
     ev_fwd = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
@@ -213,14 +217,16 @@ def main():
     valu["frac"] = valu["achieved"] / PEAK_FP32_TFLOPS
     out = {
         "metric": "transient volumes/sec (fwd+bwd), 100k Gaussians → 128×128×1024 ToF bins"
-        if a.config == "C3" else f"transient volumes/sec ({'fwd' if fwd_only else 'fwd+bwd'}) {a.config}",
+        if a.config == "C3" and (a.preset, a.mode) == ("cuda", "noocl") else f"transient volumes/sec ({'fwd' if fwd_only else 'fwd+bwd'}) {a.config}",
         "value": volumes_per_s, "unit": "volumes/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
         "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "strong" if a.shard and world > 1 else "weak", "vs_baseline": None,
         "dtype": "f32", "data": "synthetic (SURVEY §8d geometry, seeded random Gaussians and target)",
         "config": {"workload": f"{a.config}: {ng} Gaussians -> {H}x{W} wall x {T} bins, {ns}x{ns} angular "
-                               f"samples, cuda preset, no occlusion, support cutoff {a.cutoff} sigma, "
+                               f"samples, {a.preset} preset, {'no occlusion' if a.mode == 'noocl' else a.mode}, "
+                               f"{'dense (every sample)' if a.cutoff <= 0 else f'support cutoff {a.cutoff} sigma'}, "
                                f"{'fwd' if fwd_only else 'fwd+MSE+bwd (6 param grads)+Adam'}",
                    "gaussians": ng, "wall": [H, W], "bins": T, "angular": ns, "cutoff": a.cutoff,
+                   "preset": a.preset, "mode": a.mode,
                    "parallelism": (f"wall shard: {world} bands (rank r renders band r), packed grad "
                                    f"all-reduce" if a.shard and world > 1 else
                                    f"one rank's band of a {a.band}-way wall shard (projected job rate; the "
@@ -235,7 +241,7 @@ def main():
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         try:
-            out["cpu_baseline"] = cpu_baseline(a.config)
+            out["cpu_baseline"] = cpu_baseline(a.config, preset=a.preset, mode=a.mode)
         except Exception as e:  # report, never fake
             out["cpu_baseline"] = {"value": None, "error": repr(e)}
     if rank == 0:

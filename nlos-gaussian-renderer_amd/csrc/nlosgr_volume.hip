@@ -358,17 +358,32 @@ struct Drain {
     float sc, lwc, logT;  // netf: sigma c dT, log2(w c dT), log2 T at pos
     float beta, xlo, elo; // binint: dr sqrt(a/2), lower bin edge beta (kap - 1/2) and erfc(|xlo|)
     int rbase;        // RAYS: ray * nr
+    int wrap;         // dense no-occlusion: bins [0, wrap) still to drain after the first piece [start, nr)
+    float tw;         // dense no-occlusion: t at bin 0
 };
+
+// Dense no-occlusion segments span every bin, so they would all claim start bin 0 and drain in a
+// one-winner-per-round staircase.  Each bin's value is evaluated exactly (no recurrence), so a
+// segment may start anywhere: it drains [stag, nr) and then wraps to [0, stag).
+template <int MODE, bool DENSE>
+__device__ __forceinline__ constexpr bool dense_wrap() { return DENSE && MODE == NLOSGR_MODE_NOOCL; }
 
 template <int MODE, bool DENSE, bool RAYS>
 __device__ __forceinline__ bool drain_setup(const float* A, const float* u0, float lw, float sc, float lwc,
                                             float2 th, float2 ph, int i, int j, int np_, int nr, float mc2,
-                                            float r0, float dr, float inv_dr, float f0log2, Drain& d) {
+                                            float r0, float dr, float inv_dr, float f0log2, Drain& d, int stag = 0) {
     Ray R;
     if (!ray_setup<DENSE>(A, u0, th.x * ph.x, th.x * ph.y, th.y, mc2, r0, inv_dr, nr, R)) return false;
     d.pos = R.kl;
     d.rem = R.kh - R.kl + 1;
     d.t = (float)R.kl - R.ks;
+    if (dense_wrap<MODE, DENSE>()) {   // (R.kl, R.kh) = (0, nr - 1)
+        d.tw = d.t;
+        d.pos = stag;
+        d.rem = nr - stag;
+        d.wrap = stag;
+        d.t = (float)stag - R.ks;
+    }
     d.ga = -kHalfLog2e * R.a * dr * dr;
     if (MODE == NLOSGR_MODE_NOOCL) {
         d.al = fmaf(-kHalfLog2e, R.m2min, lw);
@@ -529,6 +544,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_F
     d.pos = 0; d.rem = 0; d.t = 0.f; d.ga = 0.f; d.al = 0.f; d.st = 0.f;
     d.sc = 0.f; d.lwc = 0.f; d.logT = 0.f; d.rbase = 0;
     d.beta = 0.f; d.xlo = 0.f; d.elo = 0.f;
+    d.wrap = 0; d.tw = 0.f;
     bool act = false;
     int qhead = 0, qcount = 0;
 
@@ -612,9 +628,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_F
                 const float lwcs = MODE == NLOSGR_MODE_NETF ? __shfl(lwc, slot) : 0.f;
                 bool got = false;
                 if (take && !(flags & 1)) {
+                    // dense: consecutive queue entries start 37 bins apart (distinct claim keys)
+                    const int stag = dense_wrap<MODE, DENSE>() ? (int)(((unsigned)(qhead + r) * 37u) % (unsigned)nr) : 0;
                     got = drain_setup<MODE, DENSE, RAYS>(A, u0, lws, scs, lwcs, tth[i], tph[j], i, j, np_, nr, mc2,
-                                                         r0, dr, inv_dr, f0log2, d);
-                    if (got && !(NLOSGR_DIAG && (flags & 24))) nsamp += (unsigned)d.rem;
+                                                         r0, dr, inv_dr, f0log2, d, stag);
+                    if (got && !(NLOSGR_DIAG && (flags & 24))) nsamp += (unsigned)(d.rem + (dense_wrap<MODE, DENSE>() ? d.wrap : 0));
                     act = got && !(flags & 4);    // diagnostics: segment records only
                 }
                 if (!(NLOSGR_DIAG && (flags & 8))) nseg += __popcll(__builtin_amdgcn_ballot_w64(got));
@@ -784,6 +802,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_F
                 d.elo = elo;
                 d.pos += adv;
                 d.rem -= adv;
+                if (dense_wrap<MODE, DENSE>() && d.rem <= 0 && d.wrap > 0) {   // second piece [0, wrap)
+                    d.pos = 0;
+                    d.rem = d.wrap;
+                    d.wrap = 0;
+                    d.t = d.tw;
+                }
                 act = d.rem > 0;
             }
         }
@@ -834,6 +858,132 @@ __global__ __launch_bounds__(kBlock) void hist_reduce_kernel(const float* __rest
     float s = 0.f;
     for (int sp = 0; sp < nsp; ++sp) s += hpart[(size_t)sp * P * nr + i];
     hist[i] = s * att[t] * hscale[p];
+}
+
+// Dense no-occlusion forward (cutoff <= 0: every Gaussian at every sample, the reference's own
+// support): every ray covers every bin, so the lane-serial drain above degenerates (all segments
+// claim the same bins; read-add-write chains bound by LDS latency).  Here lane = bin instead: a
+// wave walks its live pairs one at a time, computes 64 rays of the pair lane-parallel (lane = ray),
+// stages their (gamma, alpha, ks) in LDS and then, ray by ray (LDS broadcast), every lane adds the
+// exact value of its NB bins (k = lane + 64 b) into register accumulators.  No LDS writes in the
+// inner loop, no claims, fixed summation order (deterministic).
+#ifndef NLOSGR_FDREG
+#define NLOSGR_FDREG 1
+#endif
+struct FwdDenseLayout {
+    int rays, hist, total;   // offsets in floats after the float2 angle tables
+    __host__ __device__ FwdDenseLayout(int nr, int nt, int np_) {
+        const int off = al4(2 * (nt + np_));
+        rays = off;                     // float4 [kWaves][64] (gamma, alpha, ks, -)
+        hist = rays + kWaves * 64 * 4;  // [kWaves][nr]
+        total = hist + kWaves * nr;
+    }
+};
+
+template <int PRESET, int NB>
+__global__ __launch_bounds__(kBlock) void fwd_dense_kernel(KArgs k) {
+    extern __shared__ __align__(16) float smem[];
+    const int nr = k.geo.nr, nt = k.geo.nt, np_ = k.geo.np;
+    const FwdDenseLayout L(nr, nt, np_);
+    float2* tth = reinterpret_cast<float2*>(smem);
+    float2* tph = tth + nt;
+    const int wave = threadIdx.x >> 6, lane = lane_id();
+    float4* rp = reinterpret_cast<float4*>(smem + L.rays) + wave * 64;
+    const int p = blockIdx.x;
+    const int gsplit = blockIdx.y, nsp = gridDim.y;
+    const int gper = (((k.g.ng + nsp - 1) / nsp) + 63) & ~63;
+    const int g_lo = gsplit * gper, g_hi = min(k.g.ng, g_lo + gper);
+    for (int t = threadIdx.x; t < nt; t += blockDim.x)
+        tth[t] = make_float2(k.geo.sin_theta[(size_t)p * nt + t], k.geo.cos_theta[(size_t)p * nt + t]);
+    for (int t = threadIdx.x; t < np_; t += blockDim.x)
+        tph[t] = make_float2(k.geo.cos_phi[(size_t)p * np_ + t], k.geo.sin_phi[(size_t)p * np_ + t]);
+    __syncthreads();
+
+    const float px = k.geo.wall[3 * p], py = k.geo.wall[3 * p + 1], pz = k.geo.wall[3 * p + 2];
+    const float* lin = k.geo.grid_lin + 4 * (size_t)p;
+    const float r0 = k.geo.r[0];
+    const float dr = nr > 1 ? (k.geo.r[nr - 1] - r0) / (float)(nr - 1) : 0.f;
+    const float inv_dr = dr > 0.f ? 1.0f / dr : 0.f;
+    const int nray = nt * np_;
+    float acc[NB], kf[NB];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) { acc[b] = 0.f; kf[b] = (float)(lane + 64 * b); }
+
+    for (int base = g_lo + wave * 64; base < g_hi; base += kBlock) {
+        const int gi = base + lane;
+        Pair P;
+        float lw = 0.f;
+        bool live = false;
+        {
+            const int gl = min(gi, k.g.ng - 1);
+            const GaussRec rec = k.recs[gl];
+            float feat[kMaxK], mu[3];
+            load_feat(k.g, gl, feat);
+            load_rec(rec, P, mu);
+            pair_setup<PRESET, true>(k, feat, mu, px, py, pz, lin, 0.f, P);
+            live = gi < g_hi && P.w > 0.f;
+            lw = live ? flog2(P.w) : 0.f;
+        }
+        unsigned long long lm = __builtin_amdgcn_ballot_w64(live);
+        while (lm) {   // wave-uniform walk over the chunk's live pairs
+            const int sl = (int)__builtin_ctzll(lm);
+            lm &= lm - 1ull;
+            float A[9], u0[3];
+#pragma unroll
+            for (int c = 0; c < 9; ++c) A[c] = __shfl(P.A[c], sl);
+#pragma unroll
+            for (int c = 0; c < 3; ++c) u0[c] = __shfl(P.u0[c], sl);
+            const float lws = __shfl(lw, sl);
+            for (int rb = 0; rb < nray; rb += 64) {
+                const int ray = min(rb + lane, nray - 1);
+                const int i = ray / np_, j = ray - i * np_;
+                const float2 th = tth[i], ph = tph[j];
+                Ray R;
+                ray_setup<true>(A, u0, th.x * ph.x, th.x * ph.y, th.y, 0.f, r0, inv_dr, nr, R);
+                const float ga = -kHalfLog2e * R.a * dr * dr;
+                const float al = fmaf(-kHalfLog2e, R.m2min, lws) + flog2(th.x);
+                wave_sync();   // the previous batch's broadcasts are done
+                rp[lane] = make_float4(ga, al, R.ks, 0.f);
+                wave_sync();
+                const int nq = min(64, nray - rb);
+                int q = 0;
+                for (; q + 4 <= nq; q += 4) {
+                    float4 e[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) e[u] = rp[q + u];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u)
+#pragma unroll
+                        for (int b = 0; b < NB; ++b) {
+                            const float t = kf[b] - e[u].z;
+                            acc[b] += fast_exp2(fmaf(e[u].x, t * t, e[u].y));
+                        }
+                }
+                for (; q < nq; ++q) {
+                    const float4 e = rp[q];
+#pragma unroll
+                    for (int b = 0; b < NB; ++b) {
+                        const float t = kf[b] - e.z;
+                        acc[b] += fast_exp2(fmaf(e.x, t * t, e.y));
+                    }
+                }
+            }
+        }
+    }
+    float* wh = smem + L.hist + wave * nr;
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+        if (lane + 64 * b < nr) wh[lane + 64 * b] = acc[b];
+    __syncthreads();
+    const float hs = k.geo.hscale[p];
+    for (int t = threadIdx.x; t < nr; t += blockDim.x) {
+        float s = 0.f;
+        for (int w = 0; w < kWaves; ++w) s += smem[L.hist + w * nr + t];
+        if (nsp > 1)
+            k.hpart[((size_t)gsplit * k.geo.nwall + p) * nr + t] = s;
+        else
+            k.hist_out[(size_t)p * nr + t] = s * k.geo.att[t] * hs;
+    }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1814,6 +1964,37 @@ int run_fwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_
     const size_t shm = (size_t)FwdLayout(geo->nr, geo->nt, geo->np).total * sizeof(float);
     const bool dense = !(opt->cutoff > 0.f);
     const bool rays = ray_out != nullptr;
+    if (NLOSGR_FDREG && dense && !rays && !counts && hist_out && opt->mode == NLOSGR_MODE_NOOCL && geo->nr <= 1024 &&
+        !(getenv("NLOSGR_FDREG") && getenv("NLOSGR_FDREG")[0] == '0')) {
+        // dense no-occlusion histogram: lane = bin register accumulation (fwd_dense_kernel)
+        if (g->ng > 0 && geo->nwall > 0) {
+            const size_t shd = (size_t)FwdDenseLayout(geo->nr, geo->nt, geo->np).total * sizeof(float);
+            const dim3 grid(geo->nwall, ka.hpart ? ka.nfsplit : 1);
+            const int nb = (geo->nr + 63) / 64;
+            const bool tp = g->preset == NLOSGR_PRESET_TORCH;
+#define NLOSGR_FD(NBV)                                                                                   \
+    do {                                                                                                 \
+        if (tp) hipLaunchKernelGGL((fwd_dense_kernel<0, NBV>), grid, dim3(kBlock), shd, s, ka);          \
+        else hipLaunchKernelGGL((fwd_dense_kernel<1, NBV>), grid, dim3(kBlock), shd, s, ka);             \
+    } while (0)
+            if (nb <= 1) NLOSGR_FD(1);
+            else if (nb <= 2) NLOSGR_FD(2);
+            else if (nb <= 4) NLOSGR_FD(4);
+            else if (nb <= 8) NLOSGR_FD(8);
+            else NLOSGR_FD(16);
+#undef NLOSGR_FD
+            HIPCHK(hipGetLastError());
+        } else if (geo->nwall > 0) {
+            HIPCHK(hipMemsetAsync(hist_out, 0, (size_t)geo->nwall * geo->nr * sizeof(float), s));
+        }
+        if (ka.hpart && g->ng > 0 && geo->nwall > 0) {
+            const long long n = (long long)geo->nwall * geo->nr;
+            hipLaunchKernelGGL(hist_reduce_kernel, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
+                               ka.hpart, ka.nfsplit, (long long)geo->nwall, geo->nr, geo->att, geo->hscale, hist_out);
+            HIPCHK(hipGetLastError());
+        }
+        return NLOSGR_OK;
+    }
     if (g->preset == NLOSGR_PRESET_TORCH) {
         if (opt->mode == NLOSGR_MODE_NOOCL) dispatch_fwd<0, 0>(ka, dense, rays, shm, s);
         else if (opt->mode == NLOSGR_MODE_NETF) dispatch_fwd<0, 1>(ka, dense, rays, shm, s);

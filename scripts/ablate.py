@@ -8,20 +8,22 @@ from nlosgr import GaussianParams, features_flat
 from nlosgr.volume import Scene, make_config
 from nlosgr.render import render_backward, render_forward
 cfgname = sys.argv[1] if len(sys.argv) > 1 else 'C3'
-sizes = {'C3': (100_000, 128, 1024), 'S1': (20_000, 32, 512), 'C5B': (500_000, 256, 2048)}
+sizes = {'C3': (100_000, 128, 1024), 'S1': (20_000, 32, 512), 'C5B': (500_000, 256, 2048), 'C1': (1_000, 32, 128)}
+preset = os.environ.get('NLOSGR_ABLATE_PRESET', 'cuda')
+cutoff = float(os.environ.get('NLOSGR_ABLATE_CUTOFF', '3.0'))
 ng, H, T = sizes[cfgname]
 dev = torch.device('cuda:0')
 scene = Scene(H=H, W=H, T=T, ns=32)
-m = GaussianParams.synthetic(ng, 3, preset="cuda", device=dev, seed=0)
+m = GaussianParams.synthetic(ng, 3, preset=preset, device=dev, seed=0)
 if cfgname == 'C5B':   # one rank's band of the 8-way C5 wall shard
     from nlosgr.distributed import wall_band
     b0, b1 = wall_band(H * H, 0, 8)
-    geo = scene.geometry(dev, "cuda", walls=scene.walls(dev)[b0:b1].contiguous())
+    geo = scene.geometry(dev, preset, walls=scene.walls(dev)[b0:b1].contiguous())
 else:
-    geo = scene.geometry(dev, "cuda")
+    geo = scene.geometry(dev, preset)
 f = features_flat(m).detach()
 args = (m._mu.detach(), m._scaling.detach(), m._rotation.detach(), m._opacity.detach(), f, geo)
-base = make_config(m, scene, cutoff=3.0)
+base = make_config(m, scene, preset, cutoff=cutoff)
 res = {}
 for flags in (0, 4, 1, 2):
     cfg = dataclasses.replace(base, flags=flags)

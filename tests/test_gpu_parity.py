@@ -234,3 +234,27 @@ def test_bwd_shared_layout_matches_per_wave(mode, monkeypatch):
         _close(d.cpu(), b.cpu(), 1e-5, 1e-9, f"shared cached (own ws) grad {name}")
     for a, b in zip(ref_c, ref):
         _close(a.cpu(), b.cpu(), 1e-5, 1e-9, "per-wave cached")
+
+
+@pytest.mark.parametrize("preset", ["torch", "cuda"])
+@pytest.mark.parametrize("T", [40, 200])
+def test_dense_register_forward_matches_lane_serial(preset, T, monkeypatch):
+    """Dense no-occlusion histograms: the lane = bin register kernel (fwd_dense_kernel, default)
+    equals the lane-serial drain (NLOSGR_FDREG=0) within fp32 summation-order noise, for ragged
+    bin and Gaussian counts and several Gaussian splits per wall point."""
+    from nlosgr import GaussianParams, features_flat
+    from nlosgr.volume import Scene, make_config
+    from nlosgr.render import render_forward
+    dev = torch.device("cuda:0")
+    scene = Scene(H=3, W=2, T=T, ns=7)
+    m = GaussianParams.synthetic(1001, 3, preset=preset, device=dev, seed=11)
+    geo = scene.geometry(dev, preset)
+    cfg = make_config(m, scene, preset, cutoff=0.0)
+    args = (m._mu.detach(), m._scaling.detach(), m._rotation.detach(), m._opacity.detach(),
+            features_flat(m).detach().contiguous(), geo)
+    monkeypatch.delenv("NLOSGR_FDREG", raising=False)
+    h_reg, _ = render_forward(*args, cfg)
+    monkeypatch.setenv("NLOSGR_FDREG", "0")
+    h_ser, _ = render_forward(*args, cfg)
+    assert torch.isfinite(h_reg).all() and h_reg.abs().max() > 0
+    _close(h_reg.cpu(), h_ser.cpu(), FWD_RTOL, msg="register vs lane-serial")
