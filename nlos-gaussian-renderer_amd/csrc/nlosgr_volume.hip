@@ -1843,6 +1843,10 @@ int bwd_nsplit(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlos
     // (C3 backward: 2 splits 354 ms, 16 -> 309, 32 -> 305, 64 -> 302)
     int ns = (49152 + nblk - 1) / (nblk > 0 ? nblk : 1);
     if (ns > maxs) ns = maxs;
+    // per-wave layout: wave w walks wall points pbeg + w, + 4, ...; a split of fewer than 4 wall
+    // points leaves waves idle while the workgroup still holds its LDS (small walls, e.g. C1's
+    // 32x32: 1024 splits of one wall point ran one busy wave per workgroup)
+    if (!shared && ns > maxs / kWaves) ns = maxs / kWaves;
     if (ns < 1) ns = 1;
     return ns;
 }
