@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define NLOSGR_ABI_VERSION 3
+#define NLOSGR_ABI_VERSION 4
 
 /* convention presets */
 enum {
@@ -210,7 +210,8 @@ typedef struct {
 } nlosgr_adam_group;
 
 /* Volume MSE of compute_loss (nlos_helpers.py:323-327) over n elements, target scaled by gt_times:
- * loss_out[2] = {mean((hist - gt*target)^2), loss / mean((gt*target)^2)} (device floats);
+ * loss_out[4] = {mean((hist - gt*target)^2), loss / mean((gt*target)^2), sum (hist - gt*target)^2,
+ * sum (gt*target)^2} (device floats; the raw sums let the ranks of a sharded volume combine exactly);
  * grad_out [n] (may be NULL) = grad_scale * 2 (hist - gt*target) / n.  workspace: caller-owned,
  * nlosgr_mse_workspace_bytes() bytes.  Deterministic (fixed-order reduction, no atomics). */
 NLOSGR_API size_t nlosgr_mse_workspace_bytes(void);

@@ -6,7 +6,7 @@
 //   mse_kernel   : grad = grad_scale * 2 (hist - gt target) / n, and per-workgroup partial sums
 //                  of (hist - gt target)^2 and (gt target)^2; mse_finish_kernel adds the partials
 //                  in a fixed order -> loss = mean, equal_loss = loss / mean((gt target)^2)
-//                  (nlos_helpers.py:323-327).  Deterministic: no atomics.
+//                  (nlos_helpers.py:323-327), plus the two raw sums.  Deterministic: no atomics.
 //   adam_kernel  : torch.optim.Adam (no weight decay / amsgrad) with per-group learning rates and
 //                  the reference's eps = 1e-15 (gaussian_model.py:223-242); grid.y = group, so the
 //                  group descriptor is a uniform kernel-argument load.  Op order as torch:
@@ -61,6 +61,8 @@ __global__ __launch_bounds__(64) void mse_finish_kernel(const float* __restrict_
     const double loss = se / n;
     out[0] = (float)loss;
     out[1] = st > 0.0 ? (float)(loss / (st / n)) : 0.f;
+    out[2] = (float)se;   // raw sums: ranks of a sharded volume combine these, not the ratios
+    out[3] = (float)st;
 }
 
 struct AdamArgs {

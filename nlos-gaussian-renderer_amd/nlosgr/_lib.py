@@ -54,7 +54,7 @@ class AdamGroup(ctypes.Structure):
 
 ADAM_MAX_GROUPS = 8  # NLOSGR_ADAM_MAX_GROUPS
 MAX_PER_RAY = 256   # NLOSGR_MAX_PER_RAY
-ABI_VERSION = 3     # NLOSGR_ABI_VERSION
+ABI_VERSION = 4     # NLOSGR_ABI_VERSION
 
 # every symbol include/nlosgr.h declares (tests check the exports against this list)
 EXPORTS = ["nlosgr_workspace_bytes", "nlosgr_render_fwd", "nlosgr_render_bwd", "nlosgr_count_support",

@@ -15,19 +15,33 @@ PARAM_KEYS = ("mu", "features_dc", "features_rest", "opacity", "scaling", "rotat
 GROUP_ORDER = ("mu", "f_dc", "f_rest", "opacity", "scaling", "rotation")     # gaussian_model.py:229-236
 
 
-def _adam_state_dict(step):
-    """train.TrainStep's Adam as a torch.optim.Adam state_dict (group order of the reference)."""
+def _group(name, i, lr, betas=(0.9, 0.999), eps=1e-15):
+    return {"lr": float(lr), "betas": tuple(betas), "eps": float(eps), "weight_decay": 0.0, "amsgrad": False,
+            "maximize": False, "foreach": None, "capturable": False, "differentiable": False, "fused": None,
+            "name": name, "params": [i]}
+
+
+def _adam_state_dict(model, step):
+    """train.TrainStep's Adam as a torch.optim.Adam state_dict (group order of the reference,
+    gaussian_model.py:229-236).  The moments are stored in the shapes of the reference's parameter
+    tensors (features_dc [N,1,C], features_rest [N,K-1,C], opacity [N,1]; gaussian_model.py:217-221),
+    so the reference's own optimizer.load_state_dict + step accept them; TrainStep keeps flattened
+    views of the same tensors.  Without a TrainStep a fresh state (no moments yet) is written, which
+    torch.optim.Adam.load_state_dict also accepts."""
+    if step is None:
+        from .train import OptimizationParams
+        o = OptimizationParams()
+        lrs = [o.position_lr_init, o.feature_lr, o.feature_lr / 20.0, o.opacity_lr, o.scaling_lr, o.rotation_lr]
+        return {"state": {}, "param_groups": [_group(n, i, lrs[i]) for i, n in enumerate(GROUP_ORDER)]}
     adam = step.adam
     lrs = step.learning_rates(step.iteration)
     state, groups = {}, []
-    for i, name in enumerate(GROUP_ORDER):
-        p = adam.params[i]
+    for i, (name, key) in enumerate(zip(GROUP_ORDER, PARAM_KEYS)):
+        shape = getattr(model, "_" + key).shape
         state[i] = {"step": torch.tensor(float(adam.step_count)),
-                    "exp_avg": adam.exp_avg[i].detach().clone(),
-                    "exp_avg_sq": adam.exp_avg_sq[i].detach().clone()}
-        groups.append({"lr": float(lrs[i]), "betas": tuple(adam.betas), "eps": float(adam.eps), "weight_decay": 0.0,
-                       "amsgrad": False, "maximize": False, "foreach": None, "capturable": False,
-                       "differentiable": False, "fused": None, "name": name, "params": [i]})
+                    "exp_avg": adam.exp_avg[i].detach().reshape(shape).cpu().clone(),
+                    "exp_avg_sq": adam.exp_avg_sq[i].detach().reshape(shape).cpu().clone()}
+        groups.append(_group(name, i, lrs[i], adam.betas, adam.eps))
     return {"state": state, "param_groups": groups}
 
 
@@ -37,7 +51,7 @@ def save_checkpoint(path, model, train_step=None):
     ck = {k: getattr(model, "_" + k).detach().cpu() for k in PARAM_KEYS}
     ck["max_sh_degree"] = int(model.max_sh_degree)
     ck["active_sh_degree"] = int(model.active_sh_degree)
-    ck["optimizer"] = _adam_state_dict(train_step) if train_step is not None else None
+    ck["optimizer"] = _adam_state_dict(model, train_step)
     if train_step is not None:
         ck["iteration"] = int(train_step.iteration)
     torch.save(ck, path)
@@ -58,7 +72,7 @@ def load_checkpoint(path, device="cpu", train_step=None):
                 getattr(m, "_" + k).data.copy_(t[k].to(m._mu.device))
         m.active_sh_degree = int(ck["active_sh_degree"])
         opt = ck.get("optimizer")
-        if opt:
+        if opt and opt.get("state"):
             for i in range(len(GROUP_ORDER)):
                 st = opt["state"][i]
                 train_step.adam.exp_avg[i].copy_(st["exp_avg"].reshape(train_step.adam.exp_avg[i].shape))

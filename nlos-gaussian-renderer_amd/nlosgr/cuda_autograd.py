@@ -33,8 +33,8 @@ class CUDARenderFunction(torch.autograd.Function):
         ctx.nextra = len(extra)
         if not CUDA_AVAILABLE:
             raise RuntimeError("CUDA renderer not available")
-        if rendering_type not in ("netf", "nlos-neus"):
-            raise ValueError(f"unknown rendering_type {rendering_type!r}")
+        # any string is accepted: the reference maps it to 0 ('netf') / 1 (anything else) and the
+        # kernel never reads it (volume_renderer.cu:267)
         filt = gaussian_filter(ray_origins, ray_directions, gaussian_means, gaussian_scales, gaussian_rotations,
                                scaling_modifier, sigma_threshold)
         rho, dens, tr = rays_forward(ray_origins, ray_directions, t_samples, gaussian_means, gaussian_scales,

@@ -56,9 +56,10 @@ class OptimizationParams:
     opacity_reg: float = 0.01
 
 
-def mse(hist, target, gt_times=1.0, grad_scale=1.0, want_grad=True):
+def mse(hist, target, gt_times=1.0, grad_scale=1.0, want_grad=True, raw=False):
     """(loss2, grad): loss2 = device [2] = (MSE, equal_loss) of compute_loss
-    (nlos_helpers.py:323-327) against gt_times * target; grad = grad_scale * dMSE/dhist."""
+    (nlos_helpers.py:323-327) against gt_times * target; grad = grad_scale * dMSE/dhist.
+    raw=True returns the device [4] (MSE, equal_loss, sum d^2, sum (gt target)^2)."""
     lib = _lib.load()
     dev = hist.device
     h = hist.detach().contiguous()
@@ -66,11 +67,42 @@ def mse(hist, target, gt_times=1.0, grad_scale=1.0, want_grad=True):
     if h.shape != t.shape or h.dtype != torch.float32 or t.dtype != torch.float32:
         raise ValueError("nlosgr: hist and target must be float32 tensors of one shape")
     ws = torch.empty(lib.nlosgr_mse_workspace_bytes() // 4, dtype=torch.float32, device=dev)
-    out = torch.empty(2, dtype=torch.float32, device=dev)
+    out = torch.empty(4, dtype=torch.float32, device=dev)
     grad = torch.empty_like(h) if want_grad else None
     _lib.check(lib.nlosgr_mse(_lib.ptr(h), _lib.ptr(t), float(gt_times), h.numel(), float(grad_scale),
                               _lib.ptr(grad), _lib.ptr(ws), _lib.ptr(out), _lib.stream_handle(dev)))
-    return out, grad
+    return (out if raw else out[:2]), grad
+
+
+def pack_grads(grads):
+    """One contiguous fp32 buffer of the six gradient tensors (group order) and the split views."""
+    flat = torch.cat([g.reshape(-1) for g in grads])
+    views, off = [], 0
+    for g in grads:
+        views.append(flat[off:off + g.numel()].view(g.shape))
+        off += g.numel()
+    return flat, views
+
+
+def allreduce_step(grads, loss4, n_total, group=None, async_op=False):
+    """The exchange of one sharded training step: ONE all-reduce(SUM) of the packed
+    gradient buffer plus one of the two raw loss sums, then the global (MSE, equal_loss) of the
+    whole volume = (sum d^2 / n_total, sum d^2 / sum (gt t)^2) — exact for any band split, and
+    finite when a band's target is all zero.  Returns (grads, loss2) (or the work handles first when
+    async_op).  The caller's band gradients must already carry the n_local / n_total scale."""
+    flat, views = pack_grads(grads)
+    sums = loss4[2:4].clone()
+    w1 = dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group, async_op=async_op)
+    w2 = dist.all_reduce(sums, op=dist.ReduceOp.SUM, group=group, async_op=async_op)
+
+    def finish():
+        se, st = sums[0], sums[1]
+        loss = se / float(n_total)
+        eq = torch.where(st > 0, se / st, torch.zeros_like(se))
+        return views, torch.stack([loss, eq])
+    if async_op:
+        return (w1, w2), finish
+    return finish()
 
 
 class Adam:
@@ -124,6 +156,11 @@ class TrainStep:
         self.group = group
         self.world = dist.get_world_size(group) if (dist.is_available() and dist.is_initialized()) else 1
         self.n_local = geo.nwall * geo.nr
+        if nwall_total is None and self.world > 1:
+            # every rank renders its own band: the MSE normalises over the whole volume
+            t = torch.tensor([float(geo.nwall)], device=model._mu.device)
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+            nwall_total = int(t.item())
         self.n_total = (nwall_total if nwall_total is not None else geo.nwall) * geo.nr
         self.sh_schedule = sh_schedule
         self.events = events      # optional {"fwd": (start, end), "bwd": (start, end)} HIP events (bench timing)
@@ -172,7 +209,8 @@ class TrainStep:
         if ev:
             ev["fwd"][1].record(stream)
         hist, ws = out[0], (out[2] if cache else None)
-        loss2, grad = mse(hist, self.target, self.gt_times, grad_scale=self.n_local / self.n_total)
+        loss4, grad = mse(hist, self.target, self.gt_times, grad_scale=self.n_local / self.n_total, raw=True)
+        loss2 = loss4[:2]
         if ev:
             ev["bwd"][0].record(stream)
         d_mu, d_s, d_q, d_o, d_f = render_backward(*args, cfg, grad_hist=grad, workspace=ws, ray_cache=cache)
@@ -181,20 +219,7 @@ class TrainStep:
         del ws
         grads = [d_mu, d_f[:, :1], d_f[:, 1:], d_o, d_s, d_q]
         if self.world > 1:
-            flat = torch.cat([g.reshape(-1) for g in grads])
-            dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group)
-            off, split = 0, []
-            for g in grads:
-                split.append(flat[off:off + g.numel()].view(g.shape))
-                off += g.numel()
-            grads = split
-            # global loss and equal_loss from the band means (device ops; no host sync)
-            frac = self.n_local / self.n_total
-            se = loss2[0] * frac
-            st = loss2[0] / loss2[1] * frac
-            both = torch.stack([se, st])
-            dist.all_reduce(both, op=dist.ReduceOp.SUM, group=self.group)
-            loss2 = torch.stack([both[0], both[0] / both[1]])
+            grads, loss2 = allreduce_step(grads, loss4, self.n_total, self.group)
         if self.opt.regularization:
             # + opacity_reg mean|sigmoid(o)| + scale_reg mean|exp(s)| (main.py:204-208); replicated
             # terms, so added after the all-reduce.  equal_loss stays the render term's (as there).
