@@ -38,24 +38,6 @@ using namespace nlosgr;
 using namespace nlosgr::detail;
 
 // A/B switches (compile-time; defaults are the production choice)
-#ifndef NLOSGR_FWD_PF
-#define NLOSGR_FWD_PF 0        // forward: prefetch the next Gaussian chunk into registers
-#endif
-#ifndef NLOSGR_FWD_WAVES
-#define NLOSGR_FWD_WAVES 6     // forward: minimum waves per SIMD the register allocation must allow
-#endif
-#ifndef NLOSGR_PACKED
-#define NLOSGR_PACKED 0        // packed fp32 (v_pk_*) in the backward drain (measured slower: 583 vs 564 ms)
-#endif
-#ifndef NLOSGR_BWD_WAVES
-#define NLOSGR_BWD_WAVES 4     // backward: minimum waves per SIMD (4: 470 -> 444 ms at C3, few spills)
-#endif
-#ifndef NLOSGR_FPACKED
-#define NLOSGR_FPACKED 0       // packed fp32 (v_pk_*) in the forward drain
-#endif
-#ifndef NLOSGR_BWD_PF
-#define NLOSGR_BWD_PF 0        // backward: prefetch the next wall point's gradient row / tables
-#endif
 // kRecurrence: along a segment the log2 value is quadratic in the bin offset t, e(t) = ga t^2 + al,
 // so value(t+1) = value(t) * 2^(ga (2t+1)) and that ratio itself scales by 2^(2 ga) per bin.  The
 // culled drains (forward and backward, no-occlusion) re-seed value and ratio with exact exp2 once
@@ -63,49 +45,6 @@ using namespace nlosgr::detail;
 // |ga| t^2 <= m_c^2 log2(e) / 2, which bounds |ga (2t+1)| by m_c^2 log2(e) (<= 47 at m_c = 5.7),
 // so the ratio never overflows; past the segment end both factors only shrink (no inf * 0).
 // Dense mode (unbounded t) keeps the per-bin exp2.
-#ifndef NLOSGR_FREC
-#define NLOSGR_FREC 1          // forward no-occlusion drain: exp2 recurrence
-#endif
-#ifndef NLOSGR_BDECOUPLE
-#define NLOSGR_BDECOUPLE 0     // backward: lanes with a pending hand-off keep draining (measured slower: 409 vs 378 ms)
-#endif
-#ifndef NLOSGR_BDUAL
-#define NLOSGR_BDUAL 0         // backward hand-off: two claimants per pair and round (max / min lane; measured slower)
-#endif
-#ifndef NLOSGR_BPEND
-#define NLOSGR_BPEND 1         // backward: run a hand-off round once this many lanes wait
-#endif
-#ifndef NLOSGR_BVEC
-#define NLOSGR_BVEC 1          // backward no-occlusion drain: float2 reads of the gradient row
-#endif
-#ifndef NLOSGR_BGLDS
-#define NLOSGR_BGLDS 0         // backward: gradient rows copied to LDS with global_load_lds (nr % 256 == 0;
-                               // measured 302 vs 298 ms at C3: the setup phase is not bound by the row staging)
-#endif
-#ifndef NLOSGR_BRHO
-#define NLOSGR_BRHO 1          // ray cache also records each pair's albedo: the backward skips SH / footprint
-#endif
-#ifndef NLOSGR_BSENDD
-#define NLOSGR_BSENDD 0        // backward hand-off: send the ray direction (3 bpermutes) instead of its cell (slower: 290 vs 284 ms)
-#endif
-#ifndef NLOSGR_DIAG
-#define NLOSGR_DIAG 0          // utilisation counters under opt.flags 8 / 16 (scripts/drain_diag.py builds)
-#endif
-#ifndef NLOSGR_FQUAD
-#define NLOSGR_FQUAD 1         // forward culled no-occlusion drain: float4 read-add-write per 4 bins
-#endif
-#ifndef NLOSGR_FVEC
-#define NLOSGR_FVEC 2          // vector drain width: float2 (2) or float4 (4) read-add-write (C3 fwd 248 vs 282 ms)
-#endif
-#ifndef NLOSGR_FHALF
-#define NLOSGR_FHALF 0         // forward vector drain: half rounds when most winners are in their tails (slower: 233 vs 230 ms)
-#endif
-#ifndef NLOSGR_TIGHT_BOX
-#define NLOSGR_TIGHT_BOX 1     // (theta, phi) candidate box = samples inside the cap range (0: one extra sample per side)
-#endif
-#ifndef NLOSGR_BREC
-#define NLOSGR_BREC 1          // backward no-occlusion drain: exp2 recurrence + per-round moment sums
-#endif
 
 namespace {
 
@@ -126,13 +65,12 @@ struct KArgs {
     ulonglong2* cmask;           // ray cache [P][ng]: passing rays of the pair's box (bit = box cell)
     float* drho;                 // backward: dL/drho per pair [P][ng] (0 outside the support) -> sh_kernel
     float* hpart;                // forward Gaussian-split partial histograms [nfsplit][P][nr]
-    const float* growall;        // backward: dL/dhist x att x hscale rows [P][nr] (grow_kernel), or null
     float* shpart;               // sh_kernel partials [nsh][ng][kShPart]
     int nsh;                     // sh_kernel wall-point splits
     int nfsplit;                 // forward Gaussian splits per wall point (hpart != null)
     int bshared;                 // backward: 4 waves share each wall point's staged row (bwd_shared)
     unsigned* cbox;              // ray cache [P][ng]: i0 | j0 << 12 | width << 24, 0 = not cached
-    float* crho;                 // ray cache [P][ng]: the pair's SH albedo rho (NLOSGR_BRHO)
+    float* crho;                 // ray cache [P][ng]: the pair's SH albedo rho (1)
 };
 
 // ray cache: a pair whose (theta, phi) candidate box has at most 128 cells records which cells
@@ -230,8 +168,8 @@ __device__ __forceinline__ void pair_setup(const KArgs& k, const float* f, const
         const float idth = frcp(dth);
         // samples are points (theta_i = th0 + i dth): the box holds exactly the samples inside the
         // margin-widened cap range, [ceil(lo), floor(hi)] (floor/ceil added one outside row per side)
-        P.i0 = fidx(NLOSGR_TIGHT_BOX ? ceilf((thc - alpha - th0) * idth) : floorf((thc - alpha - th0) * idth), 0, nt - 1);
-        P.i1 = fidx(NLOSGR_TIGHT_BOX ? floorf((thc + alpha - th0) * idth) : ceilf((thc + alpha - th0) * idth), -1, nt - 1);
+        P.i0 = fidx(ceilf((thc - alpha - th0) * idth), 0, nt - 1);
+        P.i1 = fidx(floorf((thc + alpha - th0) * idth), -1, nt - 1);
     }
     if (thc - alpha > 1e-3f && thc + alpha < kPi - 1e-3f && dph > 0.f) {
         // max |phi - phi_c| on the cone = asin(sin(alpha) / sin(theta_c))
@@ -244,8 +182,8 @@ __device__ __forceinline__ void pair_setup(const KArgs& k, const float* f, const
             const float lo = phc - dphi, hi = phc + dphi;
             if (lo > -kPi && hi < kPi) {
                 const float idph = frcp(dph);
-                P.j0 = fidx(NLOSGR_TIGHT_BOX ? ceilf((lo - ph0) * idph) : floorf((lo - ph0) * idph), 0, np_ - 1);
-                P.j1 = fidx(NLOSGR_TIGHT_BOX ? floorf((hi - ph0) * idph) : ceilf((hi - ph0) * idph), -1, np_ - 1);
+                P.j0 = fidx(ceilf((lo - ph0) * idph), 0, np_ - 1);
+                P.j1 = fidx(floorf((hi - ph0) * idph), -1, np_ - 1);
             }
         }
     }
@@ -305,11 +243,8 @@ __device__ __forceinline__ bool ray_setup(const float* A, const float* u0, float
 // LDS carve helper (offsets in floats, 16-byte aligned)
 __host__ __device__ __forceinline__ int al4(int n) { return (n + 3) & ~3; }
 
-#ifndef NLOSGR_RQ_SMALL
-#define NLOSGR_RQ_SMALL 0
-#endif
 // ray queue ring per wave: < 64 queued + up to 64 (small ring) or 128 appended per enumeration
-constexpr int kRQ = NLOSGR_RQ_SMALL ? 128 : 256;
+constexpr int kRQ = 256;
 __device__ __forceinline__ unsigned pack_ray(int slot, int i, int j) {
     return (unsigned)slot | ((unsigned)i << 8) | ((unsigned)j << 20);
 }
@@ -323,18 +258,9 @@ __device__ __forceinline__ unsigned pack_ray(int slot, int i, int j) {
 // start bins differ — guaranteed per round by a claim table (owner[pos] = lane; losers retry
 // next round).  Lanes that did not win, or ran past their segment, point at private pad bins
 // and add 0, so the step body is branch-free.  Idle lanes are refilled from the ray queue.
-#ifndef NLOSGR_FSTEPS
-#define NLOSGR_FSTEPS 24   // with the float2 drain: 24 bins per round (C3 fwd 238 vs 243 ms at 16, 261 at 32)
-#endif
-#ifndef NLOSGR_REFILL
-#define NLOSGR_REFILL 32   // (C3: 16 -> 255, 24 -> 246, 32 -> 243, 40 -> 242, 48 -> 246 ms at 16 bins per round)
-#endif
-#ifndef NLOSGR_BREFILL
-#define NLOSGR_BREFILL 8
-#endif
-constexpr int kSteps = NLOSGR_FSTEPS;     // bins per lane per drain round
-constexpr int kRefill = NLOSGR_REFILL;    // refill once this many lanes are idle (or the queue is final)
-constexpr int kBRefill = NLOSGR_BREFILL;  // backward: same rule
+constexpr int kSteps = 24;     // bins per lane per drain round
+constexpr int kRefill = 32;    // refill once this many lanes are idle (or the queue is final)
+constexpr int kBRefill = 8;  // backward: same rule
 
 struct FwdLayout {
     int hist, owner, rayq, wave_stride, total;  // offsets in floats
@@ -412,15 +338,12 @@ __device__ __forceinline__ bool drain_setup(const float* A, const float* u0, flo
 // to the ray queue ring at qbase + cnt.  Branch-free body (every lane evaluates a clamped
 // candidate, `more` masks the result), two candidates per trip so their table reads overlap;
 // returns once cnt >= 64 or every lane exhausted its box (cnt < 64 + 2*64 <= kRQ on return).
-#ifndef NLOSGR_ENUM_NC
-#define NLOSGR_ENUM_NC 3       // candidate cells per enumeration trip (<= 3: cnt < 64 + NC*64 <= kRQ; C3 fwd 1: 234, 2: 229, 3: 227 ms)
-#endif
 template <bool DENSE, bool REC = false>
 __device__ __forceinline__ void enumerate_box(const float* M, int i1, int j0, int j1, bool& more, int& ci, int& cj,
                                               const float2* tth, const float2* tph, int nt1, unsigned* rayq,
                                               int qbase, int& cnt, unsigned long long* rec0 = nullptr,
                                               unsigned long long* rec1 = nullptr, int* cell = nullptr) {
-    constexpr int NC = NLOSGR_ENUM_NC;
+    constexpr int NC = 3;
     static_assert(NC >= 1 && 64 + NC * 64 <= kRQ, "enumeration would overflow the ray queue ring");
     const int lane = lane_id();
     do {
@@ -470,7 +393,6 @@ __device__ __forceinline__ void enumerate_box(const float* M, int i1, int j0, in
             at += __popcll(m);
         }
         cnt = at;
-        if (NLOSGR_RQ_SMALL && cnt >= 64) return;
     } while (cnt < 64 && __builtin_amdgcn_ballot_w64(more));
 }
 
@@ -499,7 +421,7 @@ __device__ __forceinline__ void enumerate_cached(unsigned long long& bits0, unsi
 __device__ __forceinline__ void compiler_fence() { __asm__ __volatile__("" ::: "memory"); }
 
 template <int PRESET, int MODE, bool DENSE, bool RAYS, bool CACHE>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_FWD_WAVES, 8))) void fwd_kernel(KArgs k) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) void fwd_kernel(KArgs k) {
     extern __shared__ __align__(16) float smem[];
     const int nr = k.geo.nr, nt = k.geo.nt, np_ = k.geo.np;
     const FwdLayout L(nr, nt, np_);
@@ -548,17 +470,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_F
     bool act = false;
     int qhead = 0, qcount = 0;
 
-#if NLOSGR_FWD_PF
-    // the next chunk's Gaussian record and feature row are fetched into registers one chunk
-    // ahead, so their latency overlaps the current chunk's enumeration and drain
-    GaussRec nrec;
-    float nfeat[kMaxK];
-    {
-        const int g0 = min(g_lo + wave * 64 + lane, k.g.ng - 1);
-        nrec = k.recs[g0];
-        load_feat(k.g, g0, nfeat);
-    }
-#endif
     for (int base = g_lo + wave * 64;; base += kBlock) {
         const bool have = base < g_hi;         // wave-uniform
         Pair P;
@@ -570,7 +481,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_F
         P.i0 = P.i1 = P.j0 = P.j1 = 0;
         if (have) {
             const int gi = base + lane;
-#if !NLOSGR_FWD_PF
             // all of the chunk's record and feature loads issued together, ahead of the setup math
             GaussRec nrec;
             float nfeat[kMaxK];
@@ -579,7 +489,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_F
                 nrec = k.recs[gl];
                 load_feat(k.g, gl, nfeat);
             }
-#endif
             if (gi < g_hi) {
                 float mu[3];
                 load_rec(nrec, P, mu);
@@ -590,17 +499,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_F
                 lwc = more ? flog2(P.w * cdt) : 0.f;
             }
             if (flags & 2) more = false;      // diagnostics: pair setup only
-            if (!(NLOSGR_DIAG && (flags & 8))) npair += __builtin_popcountll(__builtin_amdgcn_ballot_w64(more));
-            if (NLOSGR_DIAG && (flags & 16))   // diagnostics: candidate cells instead of samples
-                nsamp += more ? (unsigned)((P.i1 - P.i0 + 1) * (P.j1 - P.j0 + 1)) : 0u;
+            npair += __builtin_popcountll(__builtin_amdgcn_ballot_w64(more));
             ci = P.i0; cj = P.j0;
-#if NLOSGR_FWD_PF
-            if (base + kBlock < g_hi) {   // prefetch the next chunk
-                const int gn = min(base + kBlock + lane, k.g.ng - 1);
-                nrec = k.recs[gn];
-                load_feat(k.g, gn, nfeat);
-            }
-#endif
         }
         while (true) {
             if (qcount < 64 && __builtin_amdgcn_ballot_w64(more)) {
@@ -632,10 +532,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_F
                     const int stag = dense_wrap<MODE, DENSE>() ? (int)(((unsigned)(qhead + r) * 37u) % (unsigned)nr) : 0;
                     got = drain_setup<MODE, DENSE, RAYS>(A, u0, lws, scs, lwcs, tth[i], tph[j], i, j, np_, nr, mc2,
                                                          r0, dr, inv_dr, f0log2, d, stag);
-                    if (got && !(NLOSGR_DIAG && (flags & 24))) nsamp += (unsigned)(d.rem + (dense_wrap<MODE, DENSE>() ? d.wrap : 0));
+                    if (got) nsamp += (unsigned)(d.rem + (dense_wrap<MODE, DENSE>() ? d.wrap : 0));
                     act = got && !(flags & 4);    // diagnostics: segment records only
                 }
-                if (!(NLOSGR_DIAG && (flags & 8))) nseg += __popcll(__builtin_amdgcn_ballot_w64(got));
+                nseg += __popcll(__builtin_amdgcn_ballot_w64(got));
                 const int ntake = min(nidle, qcount);
                 qhead = (qhead + ntake) & (kRQ - 1);
                 qcount -= ntake;
@@ -647,114 +547,51 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_F
             }
             if (!anymore && qcount == 0 && have) break;   // next Gaussians; segments carry over
             // claim distinct start bins (quad drain: distinct start quads)
-            constexpr bool QUAD = NLOSGR_FQUAD && NLOSGR_FREC && MODE == NLOSGR_MODE_NOOCL && !RAYS && !DENSE;
-            constexpr int VW = NLOSGR_FVEC;   // bins per LDS read-add-write in the vector drain (4 or 2)
+            constexpr bool QUAD = MODE == NLOSGR_MODE_NOOCL && !RAYS && !DENSE;
+            constexpr int VW = 2;   // bins per LDS read-add-write of the vector drain (float2)
             const int key = QUAD ? (d.pos / VW) : d.pos;
             if (act) owner[key] = (unsigned char)lane;
             wave_sync();
             const bool win = act && owner[key] == (unsigned char)lane;
             wave_sync();
             const int remw = win ? d.rem : 0;
-            if (NLOSGR_DIAG && (flags & 8)) {   // diagnostics (count_support): rounds, active / winning lanes
-                npair += 1;
-                nseg += __popcll(__builtin_amdgcn_ballot_w64(act));
-                nsamp += __popcll(__builtin_amdgcn_ballot_w64(win));
-            }
             float* hb = hist + (win ? (QUAD ? (d.pos & ~(VW - 1)) : d.pos) : (QUAD ? padq : pad));
             float t = d.t;
             float logT = d.logT;
             float xlo = d.xlo, elo = d.elo;
-            int nsr = kSteps;   // bins this round (the vector drain may run a half round, below)
             if (QUAD) {
-                // kSteps bins from the even (VW-aligned) bin at or below pos: one ds_read_b64 +
-                // ds_write_b64 per 2 bins.  Slots before pos (first round of a segment only) add 0 and
-                // do not advance the recurrence, which starts at pos.
+                // kSteps bins from the even bin at or below pos: one ds_read_b64 + ds_write_b64 per 2
+                // bins, values by the exp2 recurrence (see kRecurrence).  Slots before pos (first round
+                // of a segment only) add 0 and do not advance the recurrence, which starts at pos.
                 const int o = d.pos & (VW - 1);
                 const int lim = remw + o;   // slot j is in the segment iff o <= j < lim
                 float cur = fast_exp2(fmaf(d.ga, t * t, d.al));
                 float q = fast_exp2(d.ga * fmaf(2.f, t, 1.f));
                 const float cc = fast_exp2(2.f * d.ga);
-                auto round_of = [&](auto ns_c) {
-                    constexpr int NS = decltype(ns_c)::value;
+                float2* hb2 = reinterpret_cast<float2*>(hb);
 #pragma unroll
-                    for (int kv = 0; kv < NS / VW; ++kv) {
-                        float v[VW];
+                for (int kv = 0; kv < kSteps / VW; ++kv) {
+                    float v[VW];
 #pragma unroll
-                        for (int jj = 0; jj < VW; ++jj) {
-                            const int j = VW * kv + jj;
-                            if (kv == 0) {
-                                const bool st = jj >= o;
-                                v[jj] = (st && j < lim) ? cur : 0.f;
-                                cur = st ? cur * q : cur;
-                                q = st ? q * cc : q;
-                            } else {
-                                v[jj] = j < lim ? cur : 0.f;
-                                cur *= q;
-                                q *= cc;
-                            }
-                        }
-                        if (VW == 4) {
-                            float4* hb4 = reinterpret_cast<float4*>(hb);
-                            float4 x = hb4[kv];
-                            x.x += v[0]; x.y += v[1]; x.z += v[2]; x.w += v[VW - 1];
-                            hb4[kv] = x;
+                    for (int jj = 0; jj < VW; ++jj) {
+                        const int j = VW * kv + jj;
+                        if (kv == 0) {
+                            const bool st = jj >= o;
+                            v[jj] = (st && j < lim) ? cur : 0.f;
+                            cur = st ? cur * q : cur;
+                            q = st ? q * cc : q;
                         } else {
-                            float2* hb2 = reinterpret_cast<float2*>(hb);
-                            float2 x = hb2[kv];
-                            x.x += v[0]; x.y += v[VW - 1];
-                            hb2[kv] = x;
+                            v[jj] = j < lim ? cur : 0.f;
+                            cur *= q;
+                            q *= cc;
                         }
-                        compiler_fence();
                     }
-                };
-                // half round when most winners would leave most of a full round empty (segment tails)
-                bool half = false;
-                if (NLOSGR_FHALF) {
-                    const int nwin = __popcll(__builtin_amdgcn_ballot_w64(win));
-                    const int nshort = __popcll(__builtin_amdgcn_ballot_w64(win && lim <= kSteps / 2));
-                    half = 2 * nshort > nwin;
-                }
-                if (half) {
-                    round_of(std::integral_constant<int, kSteps / 2>());
-                    nsr = kSteps / 2;
-                } else {
-                    round_of(std::integral_constant<int, kSteps>());
-                }
-                t += (float)(nsr - o);
-            } else if (NLOSGR_FREC && MODE == NLOSGR_MODE_NOOCL && !RAYS && !DENSE) {
-                // value(t+1) = value(t) q(t), q(t+1) = q(t) 2^(2 ga): two multiplies per bin instead of
-                // mul + fma + exp2; seeded with exact exp2 every round (see kRecurrence)
-                float cur = fast_exp2(fmaf(d.ga, t * t, d.al));
-                float q = fast_exp2(d.ga * fmaf(2.f, t, 1.f));
-                const float cc = fast_exp2(2.f * d.ga);
-#pragma unroll
-                for (int m = 0; m < kSteps; ++m) {
-                    const float v = m < remw ? cur : 0.f;
-                    cur *= q;
-                    q *= cc;
-                    const float x = hb[m];
-                    hb[m] = x + v;
+                    float2 x = hb2[kv];
+                    x.x += v[0]; x.y += v[1];
+                    hb2[kv] = x;
                     compiler_fence();
                 }
-                t += (float)kSteps;
-            } else if (NLOSGR_FPACKED && MODE == NLOSGR_MODE_NOOCL && !RAYS) {
-                // two bins per v_pk_mul/v_pk_fma/v_pk_add; the LDS read-add-write stays in bin order
-                f32x2 tv = {t, t + 1.f};
-                const f32x2 gav = {d.ga, d.ga}, alv = {d.al, d.al};
-#pragma unroll
-                for (int m = 0; m < kSteps; m += 2) {
-                    const f32x2 e = tv * tv * gav + alv;
-                    const float v0 = m < remw ? fast_exp2(e.x) : 0.f;
-                    const float v1 = m + 1 < remw ? fast_exp2(e.y) : 0.f;
-                    const float x0 = hb[m];
-                    hb[m] = x0 + v0;
-                    compiler_fence();
-                    const float x1 = hb[m + 1];
-                    hb[m + 1] = x1 + v1;
-                    compiler_fence();
-                    tv += 2.f;
-                }
-                t = tv.x;
+                t += (float)(kSteps - o);
             } else
 #pragma unroll
             for (int m = 0; m < kSteps; ++m) {
@@ -795,7 +632,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_F
                 compiler_fence();
             }
             if (win) {
-                const int adv = QUAD ? nsr - (d.pos & (NLOSGR_FVEC - 1)) : kSteps;
+                const int adv = QUAD ? kSteps - (d.pos & (VW - 1)) : kSteps;
                 d.t = t;
                 d.logT = logT;
                 d.xlo = xlo;
@@ -819,14 +656,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_F
             const bool ok = !live || bw * bh <= kCacheCells;
             k.cmask[o] = live ? make_ulonglong2(crec0, crec1) : make_ulonglong2(0ull, 0ull);
             k.cbox[o] = ok ? cache_box(live ? P.i0 : 0, live ? P.j0 : 0, live ? bw : 1) : 0u;
-            if (NLOSGR_BRHO) k.crho[o] = live ? P.rho : 0.f;
+            k.crho[o] = live ? P.rho : 0.f;
         }
         if (!have) break;
     }
     if (k.counts) {
         unsigned long long ns = nsamp;
-        if (!(NLOSGR_DIAG && (flags & 8)))
-            for (int o = 32; o > 0; o >>= 1) ns += __shfl_xor(ns, o);
+        for (int o = 32; o > 0; o >>= 1) ns += __shfl_xor(ns, o);
         if (lane == 0) {
             atomicAdd(k.counts, (unsigned long long)npair);
             atomicAdd(k.counts + 1, (unsigned long long)nseg);
@@ -867,9 +703,6 @@ __global__ __launch_bounds__(kBlock) void hist_reduce_kernel(const float* __rest
 // stages their (gamma, alpha, ks) in LDS and then, ray by ray (LDS broadcast), every lane adds the
 // exact value of its NB bins (k = lane + 64 b) into register accumulators.  No LDS writes in the
 // inner loop, no claims, fixed summation order (deterministic).
-#ifndef NLOSGR_FDREG
-#define NLOSGR_FDREG 1
-#endif
 struct FwdDenseLayout {
     int rays, hist, total;   // offsets in floats after the float2 angle tables
     __host__ __device__ FwdDenseLayout(int nr, int nt, int np_) {
@@ -995,10 +828,7 @@ __global__ __launch_bounds__(kBlock) void fwd_dense_kernel(KArgs k) {
 // its pair: finished lanes claim owner[slot] with a round stamp, each pair lane gathers its
 // claimant's result with ds_bpermute and folds it into the Gaussian's register accumulators.
 // Losers keep their result and retry next round.  No LDS float atomics, no pair/row tables.
-#ifndef NLOSGR_BSTEPS
-#define NLOSGR_BSTEPS 24   // C3 bwd: 12 -> 396, 16 -> 375, 24 -> 355, 28 -> 376, 32 -> 383 ms (spills beyond 24)
-#endif
-constexpr int kBSteps = NLOSGR_BSTEPS;   // bins per lane per backward drain round
+constexpr int kBSteps = 24;   // bins per lane per backward drain round
 constexpr int kBwdSlots = 13;   // per-Gaussian backward partial: dA[9], dMu[3], dsigma (stride 32 in HBM)
 constexpr int kShPart = 20;     // sh_kernel partial: dF[16], dMu[3], pad
 
@@ -1008,7 +838,7 @@ constexpr int kShPart = 20;     // sh_kernel partial: dF[16], dMu[3], pad
 // workgroup (staged by all 256 threads one wall point ahead, one barrier per wall point), so the
 // LDS no longer scales with 4 x nr (C5, nr = 2048: 56 KB -> 39 KB per workgroup, 2 -> 4 per CU).
 struct BwdLayout {
-    int wave_base, wave_stride, grow, tth, tph, rayq, owner, owner2, pdat, red, total, buf_stride;
+    int wave_base, wave_stride, grow, tth, tph, rayq, owner, pdat, red, total, buf_stride;
     __host__ __device__ BwdLayout(int nr, int nt, int np_, bool shared = false) {
         buf_stride = 0;
         if (shared) {
@@ -1019,8 +849,7 @@ struct BwdLayout {
             wave_base = 2 * buf_stride;
             rayq = 0;                                 // per-wave region (relative to the wave's base)
             owner = rayq + kRQ;
-            owner2 = owner + 64;
-            pdat = owner2 + (NLOSGR_BDUAL ? 64 : 0);
+            pdat = owner + 64;
             wave_stride = al4(pdat + 64 * 16);
             red = 0;                                  // unused: waves own distinct Gaussians
             total = wave_base + kWaves * wave_stride;
@@ -1032,8 +861,7 @@ struct BwdLayout {
         tph = tth + al4(2 * nt);             // float2 [np]
         rayq = tph + al4(2 * np_);           // uint [kRQ] ring
         owner = rayq + kRQ;                  // uint [64] round-stamped claims, indexed by pair slot
-        owner2 = owner + 64;                 // uint [64] second claim table (NLOSGR_BDUAL: min claim)
-        pdat = owner2 + (NLOSGR_BDUAL ? 64 : 0);   // [64][16] pair table: A[9], u0[3], w, rho, sigma, -
+        pdat = owner + 64;                   // [64][16] pair table: A[9], u0[3], w, rho, sigma, -
         wave_stride = al4(pdat + 64 * 16);
         red = wave_base;                     // final reduction reuses the wave regions
         total = wave_base + kWaves * wave_stride;
@@ -1117,45 +945,6 @@ __device__ __forceinline__ void stage_shared(const KArgs& k, int p, int nr, int 
         tph[t] = make_float2(k.geo.cos_phi[(size_t)p * np_ + t], k.geo.sin_phi[(size_t)p * np_ + t]);
 }
 
-// register prefetch of one wall point's backward inputs (see bwd_kernel)
-constexpr int kPFRow = 4;     // float4 per lane: rows up to 1024 bins
-struct RowPF {
-    float4 g[kPFRow];
-    float2 th, ph;
-    __device__ __forceinline__ void load(const KArgs& k, int p, int nr, int nt, int np_) {
-        const int lane = lane_id();
-        const float4* g4 = reinterpret_cast<const float4*>(k.grad_hist + (size_t)p * nr);
-        const int n4 = nr >> 2;
-#pragma unroll
-        for (int u = 0; u < kPFRow; ++u) {
-            const int t = lane + 64 * u;
-            g[u] = t < n4 ? g4[t] : make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-        th = lane < nt ? make_float2(k.geo.sin_theta[(size_t)p * nt + lane], k.geo.cos_theta[(size_t)p * nt + lane])
-                       : make_float2(0.f, 0.f);
-        ph = lane < np_ ? make_float2(k.geo.cos_phi[(size_t)p * np_ + lane], k.geo.sin_phi[(size_t)p * np_ + lane])
-                        : make_float2(0.f, 0.f);
-    }
-    __device__ __forceinline__ void store(const float* att, float hs, int nr, int nt, int np_, float* grow,
-                                          float2* tth, float2* tph) const {
-        const int lane = lane_id();
-        const float4* a4 = reinterpret_cast<const float4*>(att);
-        const int n4 = nr >> 2;
-#pragma unroll
-        for (int u = 0; u < kPFRow; ++u) {
-            const int t = lane + 64 * u;
-            if (t < n4) {
-                const float4 a = a4[t];
-                reinterpret_cast<float4*>(grow)[t] =
-                    make_float4(g[u].x * a.x * hs, g[u].y * a.y * hs, g[u].z * a.z * hs, g[u].w * a.w * hs);
-            }
-        }
-        for (int t = nr + lane; t < nr + kBSteps; t += 64) grow[t] = 0.f;
-        if (lane < nt) tth[lane] = th;
-        if (lane < np_) tph[lane] = ph;
-    }
-};
-
 template <int MODE, bool DENSE>
 __device__ __forceinline__ bool bray_setup(const float* pd, float2 th, float2 ph, int slot, int i, int j, int nr,
                                            float mc2, float r0, float dr, float inv_dr, float f0log2, BRay& b) {
@@ -1183,7 +972,7 @@ __device__ __forceinline__ bool bray_setup(const float* pd, float2 th, float2 ph
 }
 
 template <int PRESET, int MODE, bool DENSE, bool RAYS, bool CACHE, bool SHR>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_BWD_WAVES, 8))) void bwd_kernel(KArgs k) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) void bwd_kernel(KArgs k) {
     extern __shared__ __align__(16) float smem[];
     const int nr = k.geo.nr, nt = k.geo.nt, np_ = k.geo.np, P_ = k.geo.nwall;
     constexpr bool shr = SHR;   // == (k.bshared != 0)
@@ -1196,7 +985,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_B
     float2* tph = reinterpret_cast<float2*>(gbase + L.tph);
     unsigned* rayq = reinterpret_cast<unsigned*>(wb + L.rayq);
     unsigned* owner = reinterpret_cast<unsigned*>(wb + L.owner);
-    unsigned* owner2 = reinterpret_cast<unsigned*>(wb + L.owner2);
     float* pdat = wb + L.pdat;
 
     const int gb = blockIdx.x * (shr ? kNB * kWaves : kNB);
@@ -1216,7 +1004,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_B
     const float rscale = k.opt.ray_scale;
 
     float dA[9], dMu[3], dSig = 0.f;
-    unsigned long long dg[5] = {0ull, 0ull, 0ull, 0ull, 0ull};   // diagnostics (flags & 8)
     for (int t = 0; t < 9; ++t) dA[t] = 0.f;
     dMu[0] = dMu[1] = dMu[2] = 0.f;
     // this lane's Gaussian: record and feature row are re-read per wall point (L1/L2 hits) rather
@@ -1228,16 +1015,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_B
         mu[0] = rec.a.x; mu[1] = rec.a.y; mu[2] = rec.a.z;
     }
 
-    // software pipeline over wall points: the next wall point's upstream gradient row and
-    // angle tables are loaded into registers while this one is processed (common shapes:
-    // nr <= 1024, nr % 4 == 0, nt, np <= 64); other shapes stage synchronously
-    const bool pf = NLOSGR_BWD_PF && !shr && k.grad_hist && nr <= 4 * 64 * kPFRow && (nr & 3) == 0 && nt <= 64 && np_ <= 64 &&
-                    ((reinterpret_cast<uintptr_t>(k.grad_hist) | reinterpret_cast<uintptr_t>(k.geo.att)) & 15) == 0;
-    RowPF rpf;
-    if (pf && pbeg + wave < pend) rpf.load(k, pbeg + wave, nr, nt, np_);
-    const bool glds = NLOSGR_BGLDS && !shr && k.growall != nullptr;   // host guarantees nr % 256 == 0
-    if (glds)
-        for (int t = nr + lane; t < nr + kBSteps; t += 64) grow[t] = 0.f;   // pad: never overwritten
     if (shr && pbeg < pend) stage_shared(k, pbeg, nr, nt, np_, grow, tth, tph);
     int it = 0;
     for (int p = pbeg + (shr ? 0 : wave); p < pend; p += (shr ? 1 : kWaves), ++it) {
@@ -1255,19 +1032,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_B
             grow = bcur + L.grow;
             tth = reinterpret_cast<float2*>(bcur + L.tth);
             tph = reinterpret_cast<float2*>(bcur + L.tph);
-        } else if (glds) {
-            // 1 KiB per wave-instruction straight into LDS; retired before the drain (s_waitcnt below)
-            const float* row = k.growall + (size_t)p * nr;
-            for (int c = 0; c < nr; c += 256)
-                __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(row + c + lane * 4),
-                                                 (__attribute__((address_space(3))) void*)(grow + c), 16, 0, 0);
-            for (int t = lane; t < nt; t += 64)
-                tth[t] = make_float2(k.geo.sin_theta[(size_t)p * nt + t], k.geo.cos_theta[(size_t)p * nt + t]);
-            for (int t = lane; t < np_; t += 64)
-                tph[t] = make_float2(k.geo.cos_phi[(size_t)p * np_ + t], k.geo.sin_phi[(size_t)p * np_ + t]);
-        } else if (pf) {
-            rpf.store(k.geo.att, hs, nr, nt, np_, grow, tth, tph);
-            if (p + kWaves < pend) rpf.load(k, p + kWaves, nr, nt, np_);
         } else {
             stage_grow(k.grad_hist ? k.grad_hist + (size_t)p * nr : nullptr, k.geo.att, hs, nr, grow);
             for (int t = lane; t < nt; t += 64)
@@ -1275,8 +1039,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_B
             for (int t = lane; t < np_; t += 64)
                 tph[t] = make_float2(k.geo.cos_phi[(size_t)p * np_ + t], k.geo.sin_phi[(size_t)p * np_ + t]);
         }
-        owner[lane] = NLOSGR_BDUAL ? 0u : 0xFFFFFFFFu;
-        if (NLOSGR_BDUAL) owner2[lane] = 0xFFFFFFFFu;
+        owner[lane] = 0xFFFFFFFFu;
         const float px = k.geo.wall[3 * p], py = k.geo.wall[3 * p + 1], pz = k.geo.wall[3 * p + 2];
         // pair setup (lane = Gaussian gi at wall point p); the ray pass reads the pair table
         bool more = false;
@@ -1289,7 +1052,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_B
             float mu_[3];
             load_rec(k.recs[gi], P, mu_);
             if (CACHE) bx = k.cbox[(size_t)p * k.g.ng + gi];
-            if (CACHE && NLOSGR_BRHO && bx != 0u) {
+            if (CACHE && bx != 0u) {
                 // cached pair: u0 and the forward's albedo; no SH evaluation, no footprint (the
                 // recorded cells replace the quadric walk)
                 P.q[0] = px - mu[0]; P.q[1] = py - mu[1]; P.q[2] = pz - mu[2];
@@ -1328,7 +1091,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_B
             }
         }
         const float* gray = RAYS && k.grad_ray ? k.grad_ray + (size_t)p * nt * np_ * nr : nullptr;
-        if (glds) __builtin_amdgcn_s_waitcnt(0);   // the row copy has landed in LDS
         wave_sync();
         int ci = i0, cj = j0, qhead = 0, qcount = 0;
         unsigned round = 0;
@@ -1344,13 +1106,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_B
         b.ph1 = false;
         // pending result of a finished ray: dL/du0, dL/dv, dsigma, drho
         float rU[3] = {0.f, 0.f, 0.f}, rV[3] = {0.f, 0.f, 0.f}, rSig = 0.f, rRho = 0.f;
-        float rD[3] = {0.f, 0.f, 0.f};   // NLOSGR_BSENDD: the finished ray's direction
-#if NLOSGR_BDECOUPLE
-        int pslot = lane, pij = 0;   // pair slot and ray of the pending result
-#else
-#define pslot b.slot
-#define pij b.ij
-#endif
         while (true) {
             if (CACHE && qcount < 64 && __builtin_amdgcn_ballot_w64((cbits0 | cbits1) != 0ull)) {
                 wave_sync();
@@ -1363,13 +1118,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_B
                 wave_sync();
             }
             const bool anymore = __builtin_amdgcn_ballot_w64(more || (CACHE && (cbits0 | cbits1) != 0ull)) != 0;
-            // a lane whose finished result still waits for its hand-off keeps draining a new ray
-            // (NLOSGR_BDECOUPLE); it blocks only if that ray finishes first
-            const unsigned long long idle = __builtin_amdgcn_ballot_w64(!act && (NLOSGR_BDECOUPLE || !pend));
+            // a lane whose finished result still waits for its hand-off takes no new ray
+            const unsigned long long idle = __builtin_amdgcn_ballot_w64(!act && !pend);
             const int nidle = __popcll(idle);
             if (qcount > 0 && (nidle >= kBRefill || !anymore)) {
                 const int r = lanes_below(idle);
-                const bool take = !act && (NLOSGR_BDECOUPLE || !pend) && r < qcount;
+                const bool take = !act && !pend && r < qcount;
                 if (take && !(k.opt.flags & 1)) {                  // flags 1: enumerate only
                     const unsigned e = rayq[(qhead + r) & (kRQ - 1)];
                     const int slot = e & 0xFF, i = (e >> 8) & 0xFFF, j = e >> 20;
@@ -1386,16 +1140,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_B
                 if (!anymore && qcount == 0) break;
                 continue;
             }
-            if (NLOSGR_DIAG && (k.opt.flags & 8)) {
-                dg[0] += anyact ? 1u : 0u;
-                dg[1] += __popcll(__builtin_amdgcn_ballot_w64(act));
-            }
             if (anyact) {
                 const int remw = act ? b.rem : 0;
                 // BV: the round starts at the even bin at or below pos (float2 row reads, half the LDS
                 // instructions); slot j is bin (pos & ~1) + j, in the segment iff o <= j < remw + o
-                constexpr bool BV = NLOSGR_BVEC && MODE == NLOSGR_MODE_NOOCL && !RAYS && !DENSE && NLOSGR_BREC &&
-                                    !NLOSGR_PACKED;
+                constexpr bool BV = MODE == NLOSGR_MODE_NOOCL && !RAYS && !DENSE;
                 const int o = BV && act ? (b.pos & 1) : 0;
                 const float* gr = grow + (act ? b.pos - o : 0);
                 const float* gw = RAYS && gray ? gray + (size_t)((b.ij & 0xFFFF) * np_ + (b.ij >> 16)) * nr + b.pos
@@ -1421,26 +1170,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_B
                 }
                 float kap = b.kap;
                 if (MODE == NLOSGR_MODE_NOOCL) {
-#if NLOSGR_PACKED
-                    // two bins per instruction (v_pk_mul/fma/add_f32): even/odd partial sums
-                    f32x2 S0 = {b.S0, 0.f}, S1 = {b.S1, 0.f}, S2 = {b.S2, 0.f};
-                    f32x2 kv = {kap, kap + 1.f};
-                    const f32x2 c2 = {b.c2, b.c2}, c0 = {b.c0, b.c0};
-#pragma unroll
-                    for (int m = 0; m < kBSteps; m += 2) {
-                        const f32x2 e = kv * kv * c2 + c0;
-                        const f32x2 pv = {fast_exp2(e.x), fast_exp2(e.y)};
-                        const f32x2 H = {Hs[m], Hs[m + 1]};
-                        const f32x2 hp = H * pv;
-                        const f32x2 t1 = hp * kv;
-                        S0 += hp; S1 += t1; S2 += t1 * kv;
-                        kv += 2.f;
-                    }
-                    kap = kv.x;
-                    b.S0 = S0.x + S0.y; b.S1 = S1.x + S1.y; b.S2 = S2.x + S2.y;
-#else
                     float S0 = b.S0, S1 = b.S1, S2 = b.S2;
-                    if (NLOSGR_BREC && !DENSE) {
+                    if (!DENSE) {
                         // exp2 recurrence (kRecurrence) and moments about the round's first bin:
                         // U_n = sum_m hp m^n, then S_n += sum_m hp (kap + m)^n
                         float pdf = fast_exp2(fmaf(b.c2, kap * kap, b.c0));
@@ -1475,7 +1206,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_B
                         kap += 1.f;
                     }
                     b.S0 = S0; b.S1 = S1; b.S2 = S2;
-#endif
                 } else {
                     // dL/dD_j = c rho H_j T_j + (sum_{k>j} H_k out_k) f'_j / f_j  (two passes per ray)
                     float T = b.T, Etot = b.Etot, pre = b.pre;
@@ -1535,95 +1265,47 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_B
                             rU[r] = -zv;
                             rV[r] = -(b.ts * zv + S1 * b.zs[r] + S2 * b.v[r]);
                         }
-                        if (NLOSGR_BSENDD) {   // the ray direction travels with the result
-                            const float2 th = tth[b.ij & 0xFFFF], ph = tph[b.ij >> 16];
-                            rD[0] = th.x * ph.x; rD[1] = th.x * ph.y; rD[2] = th.y;
-                        }
-#if NLOSGR_BDECOUPLE
-                        pslot = b.slot;
-                        pij = b.ij;
-#endif
                         act = false;
                         pend = !(k.opt.flags & 32);   // flags 32 (diagnostics): drop results, no hand-off
                     }
                 }
             }
             const unsigned long long pmask = __builtin_amdgcn_ballot_w64(pend);
-            // batch hand-offs: wait for NLOSGR_BPEND pending lanes unless nothing else can run
-            if (pmask && (__popcll(pmask) >= NLOSGR_BPEND || !__builtin_amdgcn_ballot_w64(act) ||
-                          (qcount == 0 && !anymore))) {
-                // hand finished rays to their pair lanes: per pair and round one claimant (or, with
-                // NLOSGR_BDUAL, the highest and the lowest claiming lane via LDS integer max / min)
-                bool won;
-                int srcs[2];
-                bool gots[2];
-                if (NLOSGR_BDUAL) {
-                    const unsigned sA = ((round + 1u) << 8) | (unsigned)lane;
-                    const unsigned sB = ((0xFFFFFEu - round) << 8) | (unsigned)lane;
-                    if (pend) {
-                        __hip_atomic_fetch_max(owner + pslot, sA, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        __hip_atomic_fetch_min(owner2 + pslot, sB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    }
-                    wave_sync();
-                    const unsigned oA = owner[lane], oB = owner2[lane];
-                    gots[0] = (oA >> 8) == ((round + 1u) & 0xFFFFFFu);
-                    gots[1] = (oB >> 8) == ((0xFFFFFEu - round) & 0xFFFFFFu) && (oB & 63u) != (oA & 63u);
-                    srcs[0] = gots[0] ? (int)(oA & 63u) : lane;
-                    srcs[1] = gots[1] ? (int)(oB & 63u) : lane;
-                    won = pend && (owner[pslot] == sA || owner2[pslot] == sB);
+            if (pmask) {
+                // hand finished rays to their pair lanes: per pair and round one claimant (stamped
+                // claim in LDS), its result fetched by the pair lane with bpermute
+                const unsigned stamp = (round << 8) | (unsigned)lane;
+                if (pend) owner[b.slot] = stamp;
+                wave_sync();
+                const unsigned ow = owner[lane];
+                const bool got = (ow >> 8) == (round & 0xFFFFFFu);
+                const int src = got ? (int)(ow & 63u) : lane;
+                const bool won = pend && owner[b.slot] == stamp;
+                const float gm = got ? 1.f : 0.f;
+                float gU[3], gV[3];
+                // every lane must execute the bpermute: it cannot read lanes that are inactive in EXEC
+#pragma unroll
+                for (int c = 0; c < 3; ++c) { gU[c] = gm * __shfl(rU[c], src); gV[c] = gm * __shfl(rV[c], src); }
+                const float gSig = gm * __shfl(rSig, src);
+                const float gRho = MODE == NLOSGR_MODE_NOOCL ? 0.f : gm * __shfl(rRho, src);
+                const int sij = __shfl(b.ij, src);
+                const int gij = got ? sij : 0;
+                const float2 th = tth[gij & 0xFFFF], ph = tph[gij >> 16];
+                const float d3[3] = {th.x * ph.x, th.x * ph.y, th.y};
+                for (int r = 0; r < 3; ++r)
+                    for (int c = 0; c < 3; ++c) dA[3 * r + c] += gV[r] * d3[c];
+                for (int r = 0; r < 3; ++r) dU0p[r] += gU[r];
+                if (MODE == NLOSGR_MODE_NOOCL) {
+                    s0_pair += gSig;
                 } else {
-                    const unsigned stamp = (round << 8) | (unsigned)lane;
-                    if (pend) owner[pslot] = stamp;
-                    wave_sync();
-                    const unsigned o = owner[lane];
-                    gots[0] = (o >> 8) == (round & 0xFFFFFFu);
-                    gots[1] = false;
-                    srcs[0] = gots[0] ? (int)(o & 63u) : lane;
-                    srcs[1] = lane;
-                    won = pend && owner[pslot] == stamp;
-                }
-#pragma unroll
-                for (int h = 0; h < (NLOSGR_BDUAL ? 2 : 1); ++h) {
-                    const int src = srcs[h];
-                    const float gm = gots[h] ? 1.f : 0.f;
-                    float gU[3], gV[3];
-#pragma unroll
-                    for (int c = 0; c < 3; ++c) { gU[c] = gm * __shfl(rU[c], src); gV[c] = gm * __shfl(rV[c], src); }
-                    const float gSig = gm * __shfl(rSig, src);
-                    const float gRho = MODE == NLOSGR_MODE_NOOCL ? 0.f : gm * __shfl(rRho, src);
-                    // every lane must execute the bpermute: it cannot read lanes that are inactive in EXEC
-                    float d3[3];
-                    if (NLOSGR_BSENDD) {
-#pragma unroll
-                        for (int c = 0; c < 3; ++c) d3[c] = __shfl(rD[c], src);
-                    } else {
-                        const int sij = __shfl(pij, src);
-                        const int gij = gots[h] ? sij : 0;
-                        const float2 th = tth[gij & 0xFFFF], ph = tph[gij >> 16];
-                        d3[0] = th.x * ph.x; d3[1] = th.x * ph.y; d3[2] = th.y;
-                    }
-                    for (int r = 0; r < 3; ++r)
-                        for (int c = 0; c < 3; ++c) dA[3 * r + c] += gV[r] * d3[c];
-                    for (int r = 0; r < 3; ++r) dU0p[r] += gU[r];
-                    if (MODE == NLOSGR_MODE_NOOCL) {
-                        s0_pair += gSig;
-                    } else {
-                        dSig += gSig;
-                        drho_pair += gRho;
-                    }
+                    dSig += gSig;
+                    drho_pair += gRho;
                 }
                 wave_sync();
-                if (NLOSGR_DIAG && (k.opt.flags & 8)) {
-                    dg[2] += 1u;
-                    dg[3] += __popcll(__builtin_amdgcn_ballot_w64(pend));
-                    dg[4] += __popcll(__builtin_amdgcn_ballot_w64(won));
-                }
                 if (won) pend = false;
                 ++round;
             }
         }
-#undef pslot
-#undef pij
         // chain of this wall point's pair (Gaussian gi, wall point p) through u0 = A (p - mu); the
         // view-direction chain through rho (SH basis, d_features and its d_mu share) runs in
         // sh_kernel from the stored dL/drho, which keeps 16 feature accumulators out of this kernel
@@ -1643,8 +1325,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_B
         }
         if (active) k.drho[(size_t)p * k.g.ng + gi] = (wpair > 0.f && !(k.opt.flags & 64)) ? drho_pair : 0.f;
     }
-    if (NLOSGR_DIAG && (k.opt.flags & 8) && k.counts && lane == 0)
-        for (int c = 0; c < 5; ++c) atomicAdd(k.counts + c, dg[c]);
     if (shr) {   // shared layout: every wave owns its Gaussians for the whole split
         if (active) {
             float* dst = k.partial + ((size_t)split * k.g.ng + gi) * 32;
@@ -1671,18 +1351,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_B
         for (int w = 0; w < kWaves; ++w) s += red[(w * 64 + g) * kBwdSlots + c];
         k.partial[((size_t)split * k.g.ng + gb + g) * 32 + c] = s;
     }
-}
-
-// grow_kernel: the backward's per-bin weights dL/dhist[p,k] att[k] hscale[p], once per wall point,
-// so bwd_kernel can copy rows straight into LDS (global_load_lds, no VGPR staging)
-__global__ __launch_bounds__(kBlock) void grow_kernel(const float* __restrict__ grad, const float* __restrict__ att,
-                                                      const float* __restrict__ hscale, long long P, int nr,
-                                                      float* __restrict__ out) {
-    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= P * nr) return;
-    const long long p = i / nr;
-    const int t = (int)(i - p * nr);
-    out[i] = grad[i] * att[t] * hscale[p];
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1902,7 +1570,7 @@ void dispatch_bwd(const KArgs& ka, bool dense, bool rays, size_t shm, hipStream_
 // workspace layout: GaussRec[ng] | backward partials [nsplit][ng][32] | ray cache (opt->ray_cache):
 // mask 2 x u64 [P][ng] | box u32 [P][ng]
 size_t cache_bytes(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_options* opt) {
-    return opt->ray_cache ? align_up((size_t)geo->nwall * g->ng * (NLOSGR_BRHO ? 24 : 20)) : 0;
+    return opt->ray_cache ? align_up((size_t)geo->nwall * g->ng * 24) : 0;
 }
 // sh_kernel wall-point splits (>= 8 x 256-lane blocks per split row keep the chip busy at large Ng)
 int sh_nsplit(const nlosgr_gaussians* g, const nlosgr_geometry* geo) {
@@ -1912,14 +1580,11 @@ int sh_nsplit(const nlosgr_gaussians* g, const nlosgr_geometry* geo) {
     if (ns > 64) ns = 64;
     return ns < 1 ? 1 : ns;
 }
-// forward Gaussian splits per wall point: aim for NLOSGR_FWG workgroups (a 16k-workgroup grid of
+// forward Gaussian splits per wall point: aim for 131072 workgroups (a 16k-workgroup grid of
 // one long workgroup per wall point leaves a ragged last round), at least 256 Gaussians per split
-#ifndef NLOSGR_FWG
-#define NLOSGR_FWG 131072   // C3 fwd: 1 split 235 ms, 2 -> 232, 3 -> 231, 4 -> 230, 8 -> 229
-#endif
 int fwd_nsplit(const nlosgr_gaussians* g, const nlosgr_geometry* geo) {
     if (geo->nwall <= 0) return 1;
-    int ns = (NLOSGR_FWG + geo->nwall - 1) / geo->nwall;
+    int ns = (131072 + geo->nwall - 1) / geo->nwall;
     const int byg = (g->ng + 255) / 256;
     if (ns > byg) ns = byg;
     if (ns > 8) ns = 8;
@@ -1968,8 +1633,10 @@ int run_fwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_
     const size_t shm = (size_t)FwdLayout(geo->nr, geo->nt, geo->np).total * sizeof(float);
     const bool dense = !(opt->cutoff > 0.f);
     const bool rays = ray_out != nullptr;
-    if (NLOSGR_FDREG && dense && !rays && !counts && hist_out && opt->mode == NLOSGR_MODE_NOOCL && geo->nr <= 1024 &&
-        !(getenv("NLOSGR_FDREG") && getenv("NLOSGR_FDREG")[0] == '0')) {
+    // NLOSGR_FDREG=0 routes the dense histogram through fwd_kernel instead (parity cross-check in tests)
+    const char* fdreg = getenv("NLOSGR_FDREG");
+    if (dense && !rays && !counts && hist_out && opt->mode == NLOSGR_MODE_NOOCL && geo->nr <= 1024 &&
+        !(fdreg && fdreg[0] == '0')) {
         // dense no-occlusion histogram: lane = bin register accumulation (fwd_dense_kernel)
         if (g->ng > 0 && geo->nwall > 0) {
             const size_t shd = (size_t)FwdDenseLayout(geo->nr, geo->nt, geo->np).total * sizeof(float);
@@ -2030,8 +1697,7 @@ size_t nlosgr_workspace_bytes(const nlosgr_gaussians* g, const nlosgr_geometry* 
     if (validate(g, geo, opt) != NLOSGR_OK) return 0;
     const size_t rec = align_up((size_t)g->ng * sizeof(GaussRec));
     const size_t part = align_up((size_t)bwd_nsplit_ws(g, geo, opt) * g->ng * 32 * sizeof(float));
-    return rec + part + cache_bytes(g, geo, opt) + sh_bytes(g, geo) + 256 + fpart_bytes(g, geo) +
-           (NLOSGR_BGLDS ? align_up((size_t)geo->nwall * geo->nr * sizeof(float)) : 0);   // grow_kernel rows
+    return rec + part + cache_bytes(g, geo, opt) + sh_bytes(g, geo) + 256 + fpart_bytes(g, geo);
 }
 
 int nlosgr_render_fwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_options* opt,
@@ -2081,14 +1747,6 @@ int nlosgr_render_bwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo, con
         ka.drho = (float*)shb;
         ka.shpart = (float*)(shb + align_up((size_t)geo->nwall * g->ng * sizeof(float)));
         ka.nsh = sh_nsplit(g, geo);
-        if (NLOSGR_BGLDS && grad_hist && geo->nwall > 0 && (geo->nr % 256) == 0) {
-            float* rows = (float*)(shb + sh_bytes(g, geo) + 256 + fpart_bytes(g, geo));
-            const long long n = (long long)geo->nwall * geo->nr;
-            hipLaunchKernelGGL(grow_kernel, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, grad_hist,
-                               geo->att, geo->hscale, (long long)geo->nwall, geo->nr, rows);
-            HIPCHK(hipGetLastError());
-            ka.growall = rows;
-        }
         if (opt->flags & 8) {   // diagnostics: counters in the workspace's 256-B tail
             ka.counts = (unsigned long long*)(shb + sh_bytes(g, geo));
             HIPCHK(hipMemsetAsync(ka.counts, 0, 8 * sizeof(unsigned long long), s));

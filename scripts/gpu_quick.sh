@@ -4,7 +4,7 @@ export TMPDIR=/tmp
 mkdir -p gpurun_out
 timeout -k 10 300 python __graft_entry__.py smoke > gpurun_out/smoke.log 2>&1 || { echo SMOKE_FAIL $?; tail -30 gpurun_out/smoke.log; exit 1; }
 tail -1 gpurun_out/smoke.log
-timeout -k 10 900 python -m pytest tests -m gpu -q -x > gpurun_out/pytest_gpu.log 2>&1; rc=$?
+timeout -k 10 900 python -u -m pytest tests -m gpu -q -x --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1; rc=$?
 tail -15 gpurun_out/pytest_gpu.log
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python bench.py --config S1 --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/bench_s1.log 2>&1 || exit $?
