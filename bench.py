@@ -1,18 +1,31 @@
 """Benchmark: transient volumes/sec (fwd+bwd), 100k Gaussians -> 128x128x1024 ToF bins (BASELINE.json).
 
-One step = render the whole 128x128-wall-point x 1024-bin transient volume (32x32 angular
-samples per wall point, "cuda" preset, no occlusion), MSE against gt_times x a target volume,
-backward to the gradients of all six raw Gaussian parameter tensors, Adam update of the six
-parameter groups (nlosgr.train.TrainStep: the reference's learn_one_iter, main.py:198-214, over
-the whole volume).  Inputs are resident in HBM before the timed region.  With N ranks (one process per GPU, RCCL): every rank renders one full volume of
-its own capture (same scene, distinct target), gradients are summed with one all-reduce per
-step -> weak scaling, value = N volumes per step / max-over-ranks step time.
+One step = one training iteration of the reference (main.py:198-214 learn_one_iter) over the whole
+128x128-wall-point x 1024-bin transient volume (32x32 angular samples per wall point, "cuda"
+preset, no occlusion): render forward (records the ray cache) -> MSE against gt_times x a target
+volume + dL/dhist -> backward to all six raw Gaussian parameter tensors -> Adam on the six groups
+(nlosgr.train.TrainStep).  Inputs are resident in HBM before the timed region.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config C3] [--cutoff 3.0]
+Frozen workload: every step (warm-up and timed) first restores the parameters, the Adam moments and
+the iteration counter from one device snapshot (a ~34 MB device copy inside the timed region), so
+each timed step renders exactly the same Gaussians; the in-support evaluation count reported is that
+of the snapshot, i.e. of every step.
+
+Default cutoff 5.7 sigma = the parity-grade support (pdf < 1e-7 of the peak dropped;
+rel-L2 vs the 6-sigma volume 1e-7).  `--lines 3.0` adds the same step at 3 sigma (the reference
+CUDA path's sigma_threshold; rel-L2 vs dense ~3e-2) under `lines` for comparison; never `value`.
+
+With N ranks (one process per GPU, RCCL): the relay wall is split into N contiguous bands, rank r
+renders band r and the packed gradients are summed with one all-reduce per step ->
+strong scaling, value = 1 volume per step / max-over-ranks step time.  --replicas instead gives
+every rank a full volume of its own capture (weak scaling).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config C3] [--cutoff 5.7] [--lines 3.0] [--band 8] [--replicas]
 """
 import argparse
 import json
 import os
+import statistics
 import sys
 import time
 
@@ -32,84 +45,167 @@ CONFIGS = {
     "S1": (20_000, 32, 32, 512, 32, False),      # quick iteration size (not a BASELINE config)
 }
 PEAK_HBM_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-PEAK_FP32_TFLOPS = 157.3       # FP32 vector peak (the path has no MFMA shape)
-FLOP_PER_EVAL = {"fwd": 36, "bwd": 100}   # SURVEY §8d convention (FMA = 2, exp = 1)
 
 
 def param_bytes(deg):
     return 4 * (3 + 3 + 4 + 1 + (deg + 1) ** 2)        # 108 B at SH degree 3
 
 
-def cpu_baseline(cfg_name, seed=0, preset="cuda", mode="noocl"):
-    """Time the CPU oracle (dense restatement of the reference path, same preset and mode as the GPU run) on a
-    bounded sample of the same workload: 1 wall point x G_SAMPLE of the Ng Gaussians x the full
-    Ns^2 x T sample grid, fwd+bwd, in chunks of 32 Gaussians (bounded memory); extrapolated
-    linearly (the dense cost is linear in Gaussians and in wall points)."""
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(cfg_name, cutoff, seed=0, preset="cuda", mode="noocl"):
+    """The CPU oracle (oracle/torch_ref: the reference's dense torch path restated, same preset, mode
+    and support cutoff as the GPU run, so its outputs are the GPU's) on a bounded sample of the same
+    workload: WALLS wall points x G_SAMPLE of the Ng Gaussians x the full Ns^2 x T sample grid,
+    fwd+bwd.  One warm-up, then the median of 3 timed runs, on every host thread this process may
+    use (OMP_NUM_THREADS on the GPU box = its CPU share); extrapolated linearly in Gaussians and
+    wall points (the dense cost is linear in both)."""
     from nlosgr.model import GaussianParams
     from nlosgr.volume import Scene
     from oracle import torch_ref as R
     ng, H, W, T, ns, _ = CONFIGS[cfg_name]
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
     torch.set_num_threads(threads)
     scene = Scene(H=H, W=W, T=T, ns=ns)
-    g_sample = max(1, min(ng, int(os.environ.get("NLOSGR_CPU_SAMPLE_G", "160"))))
+    g_sample = max(1, min(ng, int(os.environ.get("NLOSGR_CPU_SAMPLE_G", "64"))))
     m = GaussianParams.synthetic(ng, 3, preset=preset, device="cpu", seed=seed)
     walls = scene.walls("cpu")
-    p = walls[(H // 2) * W + W // 2]
-    tab = R.sample_tables(p, scene.box("cpu"), ns, scene.start, scene.end, scene.c, scene.deltaT)
-    t0 = time.perf_counter()
-    for g0 in range(0, g_sample, 32):
-        sl = slice(g0, min(g_sample, g0 + 32))
-        P = R.Params(*(t.detach()[sl].clone() for t in (m._mu, m._scaling, m._rotation, m._opacity,
-                                                        m._features_dc, m._features_rest)), 3)
-        _, h = R.render_wallpoint(P, p, tab, 0.5, scene.c, scene.deltaT, preset=preset, mode=mode)
-        (h * h).sum().backward()
-    t = time.perf_counter() - t0
-    per_volume = t * (ng / g_sample) * (H * W)
+    pick = [(H // 4) * W + W // 4, (3 * H // 4) * W + 3 * W // 4]
+    tabs = [(walls[i], R.sample_tables(walls[i], scene.box("cpu"), ns, scene.start, scene.end, scene.c,
+                                       scene.deltaT)) for i in pick]
+    # spread the sample over the index range (synthetic Gaussians are i.i.d., so any subset is typical)
+    idx = torch.linspace(0, ng - 1, g_sample).long()
+    mc = cutoff if cutoff > 0 else None
+
+    def run():
+        t0 = time.perf_counter()
+        for g0 in range(0, g_sample, 32):
+            sl = idx[g0:g0 + 32]
+            P = R.Params(*(t.detach()[sl].clone() for t in (m._mu, m._scaling, m._rotation, m._opacity,
+                                                            m._features_dc, m._features_rest)), 3)
+            for p, tab in tabs:
+                _, h = R.render_wallpoint(P, p, tab, 0.5, scene.c, scene.deltaT, preset=preset, mode=mode, mc=mc)
+                (h * h).sum().backward()
+        return time.perf_counter() - t0
+
+    run()                                   # warm-up
+    times = [run() for _ in range(3)]
+    t = statistics.median(times)
+    per_volume = t * (ng / g_sample) * (H * W / len(pick))
     return {"value": 1.0 / per_volume, "unit": "volumes/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/torch_ref dense ({preset} preset, {mode}) fwd+bwd of 1 wall point x {g_sample} of {ng} "
-                      f"Gaussians x {ns}x{ns}x{T} samples = {t:.2f} s on {threads} threads; "
-                      f"extrapolated x{ng / g_sample:g} Gaussians x{H * W} wall points"}
+            "cpu_model": cpu_model(),
+            "sample": f"oracle/torch_ref dense ({preset} preset, {mode}, cutoff mask {cutoff} sigma) fwd+bwd of "
+                      f"{len(pick)} wall points x {g_sample} of {ng} Gaussians x {ns}x{ns}x{T} samples: median "
+                      f"of 3 after 1 warm-up = {t:.2f} s (runs {', '.join(f'{x:.2f}' for x in times)}) on "
+                      f"{threads} threads; extrapolated x{ng / g_sample:g} Gaussians x{H * W / len(pick):g} wall "
+                      f"points"}
 
 
-def pmc_traffic(cfg_name, kernels):
-    """HBM bytes per launch of `kernels` (name substrings) from the newest committed
-    profiles/r*_<cfg>_traffic.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE passes of this bench,
-    scripts/prof_c3.sh + scripts/summarize_prof.py), or None."""
+def committed_profile(cfg_name, kind, cutoff):
+    """The newest committed profiles/r*_<cfg>_<kind>.json (written by scripts/summarize_prof.py from
+    rocprofv3 passes of this bench command) recorded at the same cutoff, or (None, None)."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{cfg_name.lower()}_traffic.json")))
-    if not files:
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{cfg_name.lower()}_{kind}.json")))
+    for fn in reversed(files):
+        with open(fn) as f:
+            rec = json.load(f)
+        if rec.get("cutoff") == cutoff:
+            return rec, os.path.relpath(fn, ROOT)
+    return None, None
+
+
+def pmc_traffic(cfg_name, kernels, cutoff):
+    """HBM bytes per launch of `kernels` (name substrings): FETCH_SIZE x2 + WRITE_SIZE passes
+    (MI355X_MICROARCH.md §HBM), from the committed traffic profile, or None."""
+    rec, src = committed_profile(cfg_name, "traffic", cutoff)
+    if rec is None:
         return None, None
-    with open(files[-1]) as f:
-        rec = json.load(f)["kernels"]
     total = 0.0
     for sub in kernels:
-        hits = [v["hbm_bytes_per_launch"] for k, v in rec.items() if sub in k]
+        hits = [v["hbm_bytes_per_launch"] for k, v in rec["kernels"].items() if sub in k]
         if not hits:
             return None, None
         total += max(hits)
-    return total, os.path.relpath(files[-1], ROOT)
+    return total, src
+
+
+class Snapshot:
+    """Device copy of the trainable state (six parameter tensors, Adam moments, counters)."""
+
+    def __init__(self, train):
+        self.train = train
+        self.params = [t.clone() for t in train._tensors]
+        self.m1 = [t.clone() for t in train.adam.exp_avg]
+        self.m2 = [t.clone() for t in train.adam.exp_avg_sq]
+        self.count, self.iteration = train.adam.step_count, train.iteration
+
+    def restore(self):
+        tr = self.train
+        for dst, src in zip(tr._tensors, self.params):
+            dst.copy_(src)
+        for dst, src in zip(tr.adam.exp_avg, self.m1):
+            dst.copy_(src)
+        for dst, src in zip(tr.adam.exp_avg_sq, self.m2):
+            dst.copy_(src)
+        tr.adam.step_count, tr.iteration = self.count, self.iteration
+
+
+def timed_run(step, steps, warmup, world, dev):
+    """W untimed steps, then EXACTLY K steps between barrier + synchronize on both sides; returns
+    the max-over-ranks wall time and each step's (fwd_ms, bwd_ms) from its HIP events (read after
+    the per-step synchronize, which the driver's contract keeps inside the timed region)."""
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    phases = []
+    for _ in range(steps):
+        ev_fwd, ev_bwd = step()
+        torch.cuda.synchronize(dev)
+        phases.append((ev_fwd[0].elapsed_time(ev_fwd[1]), ev_bwd[0].elapsed_time(ev_bwd[1]) if ev_bwd else 0.0))
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    return elapsed, phases
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="C3")
-    ap.add_argument("--cutoff", type=float, default=3.0)
+    ap.add_argument("--cutoff", type=float, default=5.7,
+                    help="Mahalanobis support radius; 5.7 = parity grade (SURVEY §8d), <= 0 = dense")
+    ap.add_argument("--lines", default="",
+                    help="comma-separated extra cutoffs timed the same way (reported under 'lines'); '' = none")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--profile-json", default="")
     ap.add_argument("--preset", default="cuda", choices=("cuda", "torch"),
                     help="convention preset: cuda = the reference's CUDA path, torch = its torch path (SURVEY A.3)")
     ap.add_argument("--mode", default="noocl", choices=("noocl", "netf"),
                     help="rendering_type: noocl (configs/default.py:15 default) or netf self-transmittance")
     ap.add_argument("--band", type=int, default=0,
-                    help="render only wall band 0 of BAND equal bands (one rank's share of a BAND-GPU sharded "
-                         "volume, nlosgr.distributed.wall_band); value = projected volumes/s of the sharded job")
-    ap.add_argument("--shard", action="store_true",
-                    help="with N ranks, rank r renders wall band r of N (SURVEY §8e: one volume per step over "
-                         "the whole job, packed gradient all-reduce timed) -> strong scaling")
+                    help="single GPU: time EVERY band of a BAND-way wall shard in turn (one rank's share each); "
+                         "value = projected job rate 1 / max-over-bands step time (the all-reduce is not timed)")
+    ap.add_argument("--replicas", action="store_true",
+                    help="with N ranks: every rank renders a full volume of its own capture (weak scaling)")
     a = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -122,81 +218,88 @@ def main():
         torch.cuda.set_device(local % ndev)
         dist.init_process_group(os.environ.get("NLOSGR_DIST_BACKEND", "nccl"))
     dev = torch.device("cuda", local % ndev)
+    if a.band > 1 and world > 1:
+        raise SystemExit("--band is a single-GPU projection; with N ranks the wall is sharded by default")
 
     from nlosgr import GaussianParams
+    from nlosgr.distributed import wall_band
     from nlosgr.model import features_flat
-    from nlosgr.render import render_forward
+    from nlosgr.render import count_support, render_forward
     from nlosgr.train import TrainStep
     from nlosgr.volume import Scene, make_config
 
     ng, H, W, T, ns, fwd_only = CONFIGS[a.config]
     scene = Scene(H=H, W=W, T=T, ns=ns)
     model = GaussianParams.synthetic(ng, 3, preset=a.preset, device=dev, seed=0)
-    nwall = H * W
-    if a.shard and world > 1 and a.band > 1:
-        raise SystemExit("--band is a single-GPU projection; with N ranks use --shard")
-    band_n, band_r = (world, rank) if (a.shard and world > 1) else (a.band, 0)
-    if band_n > 1:   # one rank's contiguous band of the wall (SURVEY §8e sharding)
-        from nlosgr.distributed import wall_band
-        b0, b1 = wall_band(H * W, band_r, band_n)
-        geo = scene.geometry(dev, a.preset, a.mode, walls=scene.walls(dev)[b0:b1].contiguous())
-        nwall = b1 - b0
+    sharded = world > 1 and not a.replicas
+    walls_all = scene.walls(dev)
+    if sharded:
+        bands = [wall_band(H * W, rank, world)]
+    elif a.band > 1:
+        bands = [wall_band(H * W, r, a.band) for r in range(a.band)]
     else:
-        geo = scene.geometry(dev, a.preset, a.mode)
-    cfg = make_config(model, scene, a.preset, a.mode, cutoff=a.cutoff)
-    g = torch.Generator().manual_seed(1 + rank)
-    target = (torch.rand(nwall, T, generator=g) * 1e-3).to(dev)   # measured volume, x gt_times=100 in the loss
-    ev_fwd = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-    ev_bwd = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-    fwd_ms, bwd_ms = [], []
-    # one training iteration of the reference (main.py:198-214) over the whole volume, fused on the
-    # device: forward (records the ray cache) -> MSE vs gt_times * target + dL/dhist -> backward
-    # (walks the ray cache) -> [packed gradient all-reduce] -> Adam over the six parameter groups
-    train = TrainStep(model, geo, cfg, target, gt_times=100.0, nwall_total=H * W if band_n > 1 else H * W * world,
-                      events={"fwd": ev_fwd, "bwd": ev_bwd})
+        bands = [(0, H * W)]
+    g = torch.Generator().manual_seed(1 + (0 if sharded else rank))
+    target_all = (torch.rand(H * W, T, generator=g) * 1e-3).to(dev)   # measured volume, x gt_times=100 in the loss
     stream = torch.cuda.current_stream(dev)
+    cutoffs = [a.cutoff] + [float(x) for x in a.lines.split(",") if x.strip()]
+    results = {}
+    for cut in cutoffs:
+        cfg = make_config(model, scene, a.preset, a.mode, cutoff=cut)
+        per_band = []
+        for (b0, b1) in bands:
+            whole = (b0, b1) == (0, H * W)
+            geo = scene.geometry(dev, a.preset, a.mode, walls=None if whole else walls_all[b0:b1].contiguous())
+            target = target_all[b0:b1].contiguous()
+            ev_fwd = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+            ev_bwd = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+            train = TrainStep(model, geo, cfg, target, gt_times=100.0,
+                              nwall_total=H * W if (sharded or a.band > 1) else H * W * world,
+                              events={"fwd": ev_fwd, "bwd": ev_bwd})
+            snap = Snapshot(train)
 
-    def step(timed):
-        if fwd_only:
+            def step():
+                snap.restore()
+                if fwd_only:
+                    params = [model._mu.detach(), model._scaling.detach(), model._rotation.detach(),
+                              model._opacity.detach(), features_flat(model).detach().contiguous()]
+                    ev_fwd[0].record(stream)
+                    render_forward(*params, geo, cfg, True, False)
+                    ev_fwd[1].record(stream)
+                    return ev_fwd, None
+                train()
+                return ev_fwd, ev_bwd
+
+            elapsed, evs = timed_run(step, a.steps, a.warmup, world, dev)
+            fwd_ms = [e[0] for e in evs]
+            bwd_ms = [e[1] for e in evs] if not fwd_only else []
+            snap.restore()
             params = [model._mu.detach(), model._scaling.detach(), model._rotation.detach(),
                       model._opacity.detach(), features_flat(model).detach().contiguous()]
-            ev_fwd[0].record(stream)
-            hist, _ = render_forward(*params, geo, cfg, True, False)
-            ev_fwd[1].record(stream)
-            return hist
-        return train()
+            pairs, rays, evals = count_support(*params, geo, cfg)
+            per_band.append({"band": [b0, b1], "ms_per_step": elapsed * 1000.0 / a.steps,
+                             "fwd_ms": statistics.fmean(fwd_ms), "bwd_ms": statistics.fmean(bwd_ms) if bwd_ms else 0.0,
+                             "fwd_ms_all": fwd_ms, "bwd_ms_all": bwd_ms, "pairs": pairs, "rays": rays,
+                             "evaluations": evals, "nwall": b1 - b0})
+            del train, snap
+            torch.cuda.empty_cache()
+        results[cut] = per_band
 
-    for _ in range(a.warmup):
-        step(False)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        step(True)
-        torch.cuda.synchronize(dev)
-        fwd_ms.append(ev_fwd[0].elapsed_time(ev_fwd[1]))
-        if not fwd_only:
-            bwd_ms.append(ev_bwd[0].elapsed_time(ev_bwd[1]))
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = t.item()
-    ms_per_step = elapsed * 1000.0 / a.steps
-    # weak (replicas): every rank finishes one volume per step; sharded: the job finishes one
-    volumes_per_s = (1 if a.shard and world > 1 else world) * a.steps / elapsed
+    main_bands = results[a.cutoff]
+    worst = max(main_bands, key=lambda b: b["ms_per_step"])
+    ms_per_step = worst["ms_per_step"]
+    if sharded:
+        volumes_per_s = 1000.0 / ms_per_step
+    elif a.band > 1:
+        volumes_per_s = 1000.0 / ms_per_step          # projected: every band on its own GPU
+    else:
+        volumes_per_s = world * 1000.0 / ms_per_step
 
-    # roofline of the dominant phase (algorithmic HBM bytes / measured launch time)
+    # HBM roofline of the dominant phase: algorithmic bytes per launch / its average HIP-event
+    # duration (params read + dL/dV read + grads written for the backward)
     pb = param_bytes(3)
-    V = 4 * nwall * T
-    fwd_avg = sum(fwd_ms) / len(fwd_ms)
-    bwd_avg = sum(bwd_ms) / len(bwd_ms) if bwd_ms else 0.0
+    V = 4 * worst["nwall"] * T
+    fwd_avg, bwd_avg = worst["fwd_ms"], worst["bwd_ms"]
     if bwd_avg >= fwd_avg:
         dom, dom_ms, dom_bytes = "bwd", bwd_avg, 2 * ng * pb + V
         kern = ("preprocess_kernel", "bwd_kernel", "sh_kernel", "finish_kernel")
@@ -204,44 +307,59 @@ def main():
         dom, dom_ms, dom_bytes = "fwd", fwd_avg, ng * pb + V
         kern = ("preprocess_kernel", "fwd_kernel")
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
-    traffic, traffic_src = pmc_traffic(a.config, kern)
-    # secondary roofline: in-support evaluations (counting pass, untimed) x SURVEY FLOP convention
-    from nlosgr.render import count_support
-    params = [model._mu.detach(), model._scaling.detach(), model._rotation.detach(), model._opacity.detach(),
-              features_flat(model).detach().contiguous()]
-    pairs, rays, evals = count_support(*params, geo, cfg)
-    flops = evals * FLOP_PER_EVAL[dom]
-    valu = {"bound": "valu", "evaluations": evals, "pairs": pairs, "rays": rays,
-            "flop_per_eval": FLOP_PER_EVAL[dom], "achieved": flops / (dom_ms * 1e-3) / 1e12,
-            "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s"}
-    valu["frac"] = valu["achieved"] / PEAK_FP32_TFLOPS
+    single = a.band <= 1 and world == 1
+    traffic, traffic_src = pmc_traffic(a.config, kern, a.cutoff) if single else (None, None)
+    # compute-side figures: exact in-support evaluations of the (frozen) workload per second, and the
+    # VALU issue utilisation from the committed SQ counter pass of this command
+    # (SQ_INSTS_VALU x 2 cycles per wave64 instruction / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs))
+    valu = {"evaluations": worst["evaluations"], "pairs": worst["pairs"], "rays": worst["rays"],
+            "evals_per_s_fwd": worst["evaluations"] / (fwd_avg * 1e-3),
+            "evals_per_s_bwd": worst["evaluations"] / (bwd_avg * 1e-3) if bwd_avg else None}
+    sq, sq_src = committed_profile(a.config, "valu", a.cutoff) if single else (None, None)
+    if sq:
+        valu["valu_issue_util"] = sq.get("valu_issue_util")
+        valu["source"] = sq_src
     out = {
         "metric": "transient volumes/sec (fwd+bwd), 100k Gaussians → 128×128×1024 ToF bins"
-        if a.config == "C3" and (a.preset, a.mode) == ("cuda", "noocl") else f"transient volumes/sec ({'fwd' if fwd_only else 'fwd+bwd'}) {a.config}",
+        if a.config == "C3" and (a.preset, a.mode) == ("cuda", "noocl")
+        else f"transient volumes/sec ({'fwd' if fwd_only else 'fwd+bwd'}) {a.config}",
         "value": volumes_per_s, "unit": "volumes/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
-        "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "strong" if a.shard and world > 1 else "weak", "vs_baseline": None,
+        "ms_per_step": ms_per_step, "higher_is_better": True,
+        "scaling": "strong" if sharded else "weak", "vs_baseline": None,
         "dtype": "f32", "data": "synthetic (SURVEY §8d geometry, seeded random Gaussians and target)",
         "config": {"workload": f"{a.config}: {ng} Gaussians -> {H}x{W} wall x {T} bins, {ns}x{ns} angular "
                                f"samples, {a.preset} preset, {'no occlusion' if a.mode == 'noocl' else a.mode}, "
                                f"{'dense (every sample)' if a.cutoff <= 0 else f'support cutoff {a.cutoff} sigma'}, "
-                               f"{'fwd' if fwd_only else 'fwd+MSE+bwd (6 param grads)+Adam'}",
+                               f"{'fwd' if fwd_only else 'fwd+MSE+bwd (6 param grads)+Adam'}, frozen workload",
                    "gaussians": ng, "wall": [H, W], "bins": T, "angular": ns, "cutoff": a.cutoff,
                    "preset": a.preset, "mode": a.mode,
-                   "parallelism": (f"wall shard: {world} bands (rank r renders band r), packed grad "
-                                   f"all-reduce" if a.shard and world > 1 else
-                                   f"one rank's band of a {a.band}-way wall shard (projected job rate; the "
-                                   f"packed gradient all-reduce is not timed)" if a.band > 1 else
-                                   f"wall-replica x{world}, grad all-reduce" if world > 1 else "single GPU")},
+                   "parallelism": (f"wall shard: {world} bands (rank r renders band r), packed grad all-reduce"
+                                   if sharded else
+                                   f"all {a.band} bands of a {a.band}-way wall shard timed in turn on one GPU "
+                                   f"(projected job rate = 1 / slowest band; all-reduce not timed)" if a.band > 1 else
+                                   f"replicas x{world} (own capture each), grad all-reduce" if world > 1 else
+                                   "single GPU")},
         "phase_ms": {"fwd": fwd_avg, "bwd": bwd_avg},
         "roofline": {"bound": "hbm", "kernel": f"nlosgr {dom} ({' + '.join(kern)})", "achieved": achieved,
                      "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS,
                      "traffic": traffic, "traffic_source": traffic_src,
                      "algorithmic_bytes_per_launch": dom_bytes, "avg_launch_ms": dom_ms},
-        "roofline_valu": valu,
+        "compute": valu,
     }
+    if a.band > 1:
+        out["bands"] = [{k: b[k] for k in ("band", "ms_per_step", "fwd_ms", "bwd_ms", "evaluations")}
+                        for b in main_bands]
+    lines = []
+    for cut in cutoffs[1:]:
+        b = max(results[cut], key=lambda x: x["ms_per_step"])
+        lines.append({"cutoff": cut, "value": (1 if (sharded or a.band > 1) else world) * 1000.0 / b["ms_per_step"],
+                      "ms_per_step": b["ms_per_step"], "phase_ms": {"fwd": b["fwd_ms"], "bwd": b["bwd_ms"]},
+                      "evaluations": b["evaluations"]})
+    if lines:
+        out["lines"] = lines
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         try:
-            out["cpu_baseline"] = cpu_baseline(a.config, preset=a.preset, mode=a.mode)
+            out["cpu_baseline"] = cpu_baseline(a.config, a.cutoff, preset=a.preset, mode=a.mode)
         except Exception as e:  # report, never fake
             out["cpu_baseline"] = {"value": None, "error": repr(e)}
     if rank == 0:

@@ -98,9 +98,8 @@ def render_rays(ray_origins, ray_directions, t_samples, gaussian_means, gaussian
                 gaussian_opacities, gaussian_features, camera_pos, active_sh_degree, c, deltaT, scaling_modifier,
                 use_occlusion, rendering_type="netf", sigma_threshold=3.0, preset="cuda"):
     """_C.render_rays (non-differentiable; volume_renderer.cu:189-305): boxes, filter, render.
-    rendering_type is accepted and, as in the reference kernel, does not change the result."""
-    if rendering_type not in ("netf", "nlos-neus"):
-        raise ValueError(f"unknown rendering_type {rendering_type!r}")
+    rendering_type is accepted (any string; the reference maps it to an int it never reads,
+    volume_renderer.cu:267) and does not change the result."""
     filt = gaussian_filter(ray_origins, ray_directions, gaussian_means, gaussian_scales, gaussian_rotations,
                            scaling_modifier, sigma_threshold, preset)
     return rays_forward(ray_origins, ray_directions, t_samples, gaussian_means, gaussian_scales,
@@ -115,8 +114,6 @@ def render_rays_analytic(ray_origins, ray_directions, t_min, t_max, gaussian_fil
     one value per ray from the sections of the filtered Gaussians.  c, deltaT and rendering_type
     are accepted and unused, as in the reference kernel.  Forward only (the reference has no
     backward for this path)."""
-    if rendering_type not in ("netf", "nlos-neus"):
-        raise ValueError(f"unknown rendering_type {rendering_type!r}")
     lib = _lib.load()
     ro, rd, cam = [_as_f32(x) for x in (ray_origins, ray_directions, camera_pos)]
     means, scales, rotations, opacities, features = [_as_f32(x) for x in (gaussian_means, gaussian_scales,

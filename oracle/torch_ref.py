@@ -311,6 +311,17 @@ def bboxes_cuda(P, mod=1.0, sigma=3.0):
     return torch.cat([P._mu - ext, P._mu + ext], dim=1)
 
 
+def bboxes_torch(P, mod=1.0, sigma=3.0):
+    """gaussian_model.py:140-178 GaussianModel.get_bboxes — [Ng, 6]: L = build_rotation(normalize(q)) @
+    diag(exp(S) mod) (gaussian_utils.py:212-221), extent = sigma sqrt(clamp_min(diag(L Lᵀ), 1e-8))."""
+    s = torch.exp(P._scaling) * mod
+    R = build_rotation(torch.nn.functional.normalize(P._rotation))
+    L = R * s[:, None, :]
+    cov = L @ L.transpose(1, 2)
+    ext = sigma * torch.sqrt(torch.clamp_min(torch.diagonal(cov, dim1=-2, dim2=-1), 1e-8))
+    return torch.cat([P._mu - ext, P._mu + ext], dim=1)
+
+
 def aabb_filter(ray_o, ray_d, bboxes, cap=256):
     """ray_aabb.cu:10-61 + cuda_utils.cuh:97-121 — int32 [N_rays, cap+1]: count, then the first
     `cap` Gaussian indices (index order) whose box the half-infinite ray hits, -1 padding."""

@@ -1,10 +1,18 @@
-"""Summarise a prof_c3.sh run into profiles/: per-kernel stats (copied) and per-launch HBM traffic
-from the FETCH_SIZE / WRITE_SIZE passes (FETCH_SIZE doubled: MI355X_MICROARCH.md §HBM, gfx950
-reports half the bytes of wide reads; WRITE_SIZE taken as is).  FETCH/WRITE_SIZE are in KB.
+"""Summarise a prof_c3.sh run into profiles/ (all per launch, averaged over the run's launches):
+  <tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (copied)
+  <tag>_traffic.json       HBM bytes = FETCH_SIZE x2 + WRITE_SIZE (MI355X_MICROARCH.md §HBM: gfx950
+                           reports half the bytes of wide reads; WRITE_SIZE as is; both in KB)
+  <tag>_valu.json          SQ + GRBM pass: VALU issue utilisation = SQ_INSTS_VALU x 2 cycles per
+                           wave64 instruction / (128 SIMDs per XCD x GRBM_GUI_ACTIVE), GRBM_GUI_ACTIVE
+                           being the sum over the 8 XCDs of each XCD's busy cycles (so 1024 SIMDs x
+                           GRBM/8).  Transcendentals issue for longer, so this is a lower bound.
+  <tag>_sq_counters.csv    the raw SQ/GRBM rows of this library's kernels
+  <tag>_bench.json         the bench line of the same command
 
-    python scripts/summarize_prof.py gpurun_out/prof_c3 r01_c3
+    python scripts/summarize_prof.py gpurun_out/prof_c3 r02_c3
 """
 import csv
+import glob
 import json
 import os
 import shutil
@@ -14,43 +22,71 @@ from collections import defaultdict
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def per_kernel(path, counter):
-    acc = defaultdict(list)
+def per_kernel(path):
+    acc = defaultdict(lambda: defaultdict(list))
     with open(path) as f:
         for row in csv.DictReader(f):
-            if row["Counter_Name"] == counter:
-                acc[row["Kernel_Name"]].append(float(row["Counter_Value"]))
+            acc[row["Kernel_Name"]][row["Counter_Name"]].append(float(row["Counter_Value"]))
     return acc
+
+
+def ours(k):
+    return "anonymous namespace" in k or "nlosgr" in k
+
+
+def short(k):
+    return k.replace("(anonymous namespace)::", "").replace("nlosgr::detail::", "").split("(")[0]
 
 
 def main(src, tag):
     out = os.path.join(ROOT, "profiles")
     os.makedirs(out, exist_ok=True)
-    stats = [f for f in os.listdir(src) if f.startswith("kt_") and f.endswith("kernel_stats.csv")]
-    for f in stats:
-        shutil.copy(os.path.join(src, f), os.path.join(out, f"{tag}_kernel_stats.csv"))
-    fetch = per_kernel(os.path.join(src, "fetch_c3_counter_collection.csv"), "FETCH_SIZE")
-    write = per_kernel(os.path.join(src, "write_c3_counter_collection.csv"), "WRITE_SIZE")
+    bench = open(os.path.join(src, "bench_default.log")).read().strip().splitlines()[-1]
+    line = json.loads(bench)
+    cutoff = line["config"]["cutoff"]
+    with open(os.path.join(out, f"{tag}_bench.json"), "w") as f:
+        f.write(bench + "\n")
+    for f in glob.glob(os.path.join(src, "kt_*kernel_stats.csv")):
+        shutil.copy(f, os.path.join(out, f"{tag}_kernel_stats.csv"))
+    fetch = per_kernel(glob.glob(os.path.join(src, "fetch_*counter_collection.csv"))[0])
+    write = per_kernel(glob.glob(os.path.join(src, "write_*counter_collection.csv"))[0])
     res = {}
     for k in sorted(set(fetch) | set(write)):
-        if "rocclr" in k or "elementwise" in k.lower() or "at::" in k:
+        if not ours(k):
             continue
-        fb = 2.0 * 1024 * sum(fetch.get(k, [0])) / max(1, len(fetch.get(k, [1])))
-        wb = 1024 * sum(write.get(k, [0])) / max(1, len(write.get(k, [1])))
-        res[k] = {"fetch_bytes_x2": fb, "write_bytes": wb, "hbm_bytes_per_launch": fb + wb,
-                  "launches": max(len(fetch.get(k, [])), len(write.get(k, [])))}
-    sq = os.path.join(src, "sq_c3_counter_collection.csv")
-    if os.path.exists(sq):   # keep only this library's kernels
-        with open(sq) as f, open(os.path.join(out, f"{tag}_sq_counters.csv"), "w", newline="") as g:
+        fl, wl = fetch.get(k, {}).get("FETCH_SIZE", []), write.get(k, {}).get("WRITE_SIZE", [])
+        fb = 2.0 * 1024 * sum(fl) / max(1, len(fl))
+        wb = 1024 * sum(wl) / max(1, len(wl))
+        res[short(k)] = {"fetch_bytes_x2": fb, "write_bytes": wb, "hbm_bytes_per_launch": fb + wb,
+                         "launches": max(len(fl), len(wl))}
+    with open(os.path.join(out, f"{tag}_traffic.json"), "w") as f:
+        json.dump({"source": f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE passes of bench.py ({tag})",
+                   "cutoff": cutoff, "kernels": res}, f, indent=1)
+    sqf = glob.glob(os.path.join(src, "sq_*counter_collection.csv"))
+    if sqf:
+        sq = per_kernel(sqf[0])
+        kern = {}
+        for k, c in sq.items():
+            if not ours(k):
+                continue
+            avg = {n: sum(v) / len(v) for n, v in c.items()}
+            g = avg.get("GRBM_GUI_ACTIVE", 0.0)
+            avg["valu_issue_util"] = 2.0 * avg.get("SQ_INSTS_VALU", 0.0) / (128.0 * g) if g else None
+            avg["launches"] = max(len(v) for v in c.values())
+            kern[short(k)] = avg
+        dom = max((v for k, v in kern.items() if "fwd_kernel" in k or "bwd_kernel" in k),
+                  key=lambda v: v.get("GRBM_GUI_ACTIVE", 0.0), default=None)
+        with open(os.path.join(out, f"{tag}_valu.json"), "w") as f:
+            json.dump({"source": f"rocprofv3 --pmc SQ_* GRBM_GUI_ACTIVE pass of bench.py ({tag})",
+                       "cutoff": cutoff, "formula": "2 * SQ_INSTS_VALU / (128 * GRBM_GUI_ACTIVE)",
+                       "valu_issue_util": dom["valu_issue_util"] if dom else None, "kernels": kern}, f, indent=1)
+        with open(sqf[0]) as f, open(os.path.join(out, f"{tag}_sq_counters.csv"), "w", newline="") as g:
             rd = csv.DictReader(f)
             wr = csv.DictWriter(g, fieldnames=rd.fieldnames)
             wr.writeheader()
             for row in rd:
-                if "anonymous namespace" in row["Kernel_Name"]:
+                if ours(row["Kernel_Name"]):
                     wr.writerow(row)
-    with open(os.path.join(out, f"{tag}_traffic.json"), "w") as f:
-        json.dump({"source": f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE passes of bench.py ({tag})",
-                   "kernels": res}, f, indent=1)
     for k, v in res.items():
         print(f"{v['hbm_bytes_per_launch'] / 1e6:10.2f} MB  {k[:90]}")
 

@@ -5,6 +5,7 @@ import os
 import re
 
 import numpy as np
+import pytest
 import torch
 
 from conftest import ROOT
@@ -83,3 +84,17 @@ def test_geometry_slice_and_wall_grid():
     geo = build_geometry(walls, volume_box_point((0, 0.5, 0), 0.5), 8, 4, 36, 1.0, 0.04, 0.5, "cuda")
     s = geo.slice(6, 12)
     assert s.nwall == 6 and torch.equal(s.wall, geo.wall[6:12]) and s.nr == 32
+
+
+def test_dropin_renderers_fail_loudly_without_gpu():
+    """The reference's package front (submodules/cuda_renderer/__init__.py) raises when its
+    extension is missing; the drop-ins do the same here without a GPU instead of falling back."""
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from nlosgr import cuda_renderer
+    assert cuda_renderer.MAX_GAUSSIANS_PER_RAY == 256
+    assert cuda_renderer.CUDA_AVAILABLE is False
+    with pytest.raises(RuntimeError):
+        cuda_renderer.create_renderer(3.0)
+    with pytest.raises(RuntimeError):
+        cuda_renderer.NLOSGaussianRenderer()

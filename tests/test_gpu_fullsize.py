@@ -1,0 +1,225 @@
+"""BASELINE configurations at full size on the GPU (C1, C2, C3, C4, one C5 band).
+
+The CPU oracle cannot render a whole C2/C3/C5 volume, so each full-size run is checked three ways:
+  * the whole volume (and, where the config trains, every gradient) is finite, and the
+    no-occlusion histograms are non-negative;
+  * sampled wall points against the oracle (oracle/torch_ref, golden-pinned for the torch preset)
+    at full geometry: C1 with all 1,000 Gaussians; C2/C3/C5 with a Gaussian subset rendered by the
+    HIP path on the full-size geometry tables;
+  * the parity-grade culled run (cutoff 5.7 sigma, the bench default) against the exact dense HIP
+    evaluation (cutoff 0, itself pinned to the oracle in test_gpu_parity.py) on sampled wall points,
+    forward and backward (gradients seeded on those points only).
+Tolerances: forward max|a-b| <= 2e-5 max|b| (+1e-7 abs) vs the oracle and 1e-5 for culled vs dense;
+gradients 2e-4 of each tensor's max.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import ROOT  # noqa: F401
+
+pytestmark = pytest.mark.gpu
+
+PARITY_CUTOFF = 5.7
+
+
+def _close(a, b, rtol, atol=1e-7, msg=""):
+    a = np.asarray(a.detach().cpu() if torch.is_tensor(a) else a, dtype=np.float64)
+    b = np.asarray(b.detach().cpu() if torch.is_tensor(b) else b, dtype=np.float64)
+    scale = np.abs(b).max() if b.size else 0.0
+    err = np.abs(a - b).max() if b.size else 0.0
+    assert err <= rtol * scale + atol, f"{msg}: max err {err:.3e} vs scale {scale:.3e}"
+
+
+def _params(m):
+    from nlosgr import features_flat
+    return [m._mu.detach(), m._scaling.detach(), m._rotation.detach(), m._opacity.detach(),
+            features_flat(m).detach().contiguous()]
+
+
+def _subset(m, idx):
+    from nlosgr import GaussianParams
+    return GaussianParams(*(t.detach()[idx].clone() for t in (m._mu, m._scaling, m._rotation, m._opacity,
+                                                               m._features_dc, m._features_rest)),
+                          m.active_sh_degree, m.max_sh_degree)
+
+
+def _oracle(m, scene, walls_idx, preset, mode, mc, gout=None, chunk=50):
+    """oracle hist [len(walls_idx), T] of model m at the scene's full geometry, Gaussians in chunks
+    (bounded memory); with gout [len(walls_idx), T] also d(sum gout*hist)/d(six raw tensors)."""
+    from oracle import torch_ref as R
+    cpu = [t.detach().cpu() for t in (m._mu, m._scaling, m._rotation, m._opacity, m._features_dc,
+                                       m._features_rest)]
+    walls = scene.walls("cpu")[walls_idx]
+    box = scene.box("cpu")
+    ng = cpu[0].shape[0]
+    hist = None
+    grads = [torch.zeros_like(t) for t in cpu]
+    for g0 in range(0, ng, chunk):
+        P = R.Params(*(t[g0:g0 + chunk] for t in cpu), m.active_sh_degree, requires_grad=gout is not None)
+        h = R.render_volume(P, walls, box, scene.volume_position[1], scene.ns, scene.start, scene.end, scene.c,
+                            scene.deltaT, preset=preset, mode=mode, mc=mc)
+        if gout is not None:
+            (h * gout).sum().backward()
+            for gacc, leaf in zip(grads, P.leaves()):
+                gacc[g0:g0 + chunk] = leaf.grad
+        hist = h.detach() if hist is None else hist + h.detach()
+    return hist, grads
+
+
+def _hip_grads_as_ref(d):
+    """HIP (d_mu, d_s, d_q, d_o, d_f[Ng,K]) -> the reference's six tensors' shapes (dc, rest split)."""
+    d_mu, d_s, d_q, d_o, d_f = d
+    return [d_mu, d_s, d_q, d_o.reshape(-1, 1), d_f[:, :1].reshape(-1, 1, 1), d_f[:, 1:].reshape(d_f.shape[0], -1, 1)]
+
+
+def _finite_volume(hist, nonneg=True):
+    assert torch.isfinite(hist).all(), "non-finite volume"
+    if nonneg:
+        assert float(hist.min()) >= 0.0, f"negative histogram value {float(hist.min()):.3e}"
+
+
+def _culled_vs_dense(m, scene, preset, idx, hist_culled, grads_culled=None, gseed=None):
+    """hist rows idx of the full culled run vs the dense HIP evaluation of those wall points;
+    with grads_culled (full-volume backward seeded with gseed on rows idx only) also the gradients."""
+    from nlosgr.render import render_backward, render_forward
+    from nlosgr.volume import make_config
+    dev = hist_culled.device
+    geo = scene.geometry(dev, preset, "noocl", walls=scene.walls(dev)[idx].contiguous())
+    cfg = make_config(m, scene, preset, "noocl", cutoff=0.0)
+    ref, _ = render_forward(*_params(m), geo, cfg)
+    _close(hist_culled[idx], ref, 1e-5, msg="culled 5.7 sigma vs dense hist")
+    if grads_culled is not None:
+        dref = render_backward(*_params(m), geo, cfg, grad_hist=gseed)
+        for name, a, b in zip(("mu", "scaling", "rotation", "opacity", "features"), grads_culled, dref):
+            _close(a, b, 2e-4, atol=1e-9, msg=f"culled vs dense grad {name}")
+
+
+def test_c1_full_size():
+    """C1: 1k Gaussians -> 32x32 wall x 128 bins, 32x32 angular samples, torch preset (path T, the
+    golden-pinned convention), dense.  Whole volume on the GPU; 8 spread wall points (every
+    Gaussian) and their gradients against the oracle."""
+    from nlosgr import GaussianParams
+    from nlosgr.render import render_backward, render_forward
+    from nlosgr.volume import Scene, make_config
+    dev = torch.device("cuda:0")
+    scene = Scene(H=32, W=32, T=128, ns=32)
+    m = GaussianParams.synthetic(1000, 3, preset="torch", device=dev, seed=0)
+    geo = scene.geometry(dev, "torch", "noocl")
+    cfg = make_config(m, scene, "torch", "noocl", cutoff=0.0)
+    hist, _ = render_forward(*_params(m), geo, cfg)
+    assert hist.shape == (32 * 32, 128)
+    _finite_volume(hist)
+    idx = torch.tensor([0, 31, 100, 333, 528, 777, 992, 1023])
+    g = torch.Generator().manual_seed(7)
+    gout = torch.randn(len(idx), 128, generator=g)
+    gfull = torch.zeros(32 * 32, 128)
+    gfull[idx] = gout
+    d = render_backward(*_params(m), geo, cfg, grad_hist=gfull.to(dev))
+    for t in d:
+        assert torch.isfinite(t).all()
+    ref, rgrads = _oracle(m, scene, idx, "torch", "noocl", None, gout=gout)
+    _close(hist[idx.to(dev)], ref, 2e-5, msg="C1 hist")
+    for name, a, b in zip(("mu", "scaling", "rotation", "opacity", "dc", "rest"), _hip_grads_as_ref(d), rgrads):
+        _close(a, b, 2e-4, atol=1e-9, msg=f"C1 grad {name}")
+
+
+def test_c2_full_size():
+    """C2: 50k Gaussians -> 64x64 wall x 512 bins, forward only, cuda preset, cutoff 5.7 sigma."""
+    from nlosgr import GaussianParams
+    from nlosgr.render import render_forward
+    from nlosgr.volume import Scene, make_config
+    dev = torch.device("cuda:0")
+    scene = Scene(H=64, W=64, T=512, ns=32)
+    m = GaussianParams.synthetic(50_000, 3, preset="cuda", device=dev, seed=0)
+    geo = scene.geometry(dev, "cuda", "noocl")
+    cfg = make_config(m, scene, "cuda", "noocl", cutoff=PARITY_CUTOFF)
+    hist, _ = render_forward(*_params(m), geo, cfg)
+    assert hist.shape == (64 * 64, 512)
+    _finite_volume(hist)
+    assert float(hist.sum()) > 0
+    idx = torch.tensor([0, 1000, 2080, 4095])
+    _culled_vs_dense(m, scene, "cuda", idx.to(dev), hist)
+    # a Gaussian subset on the full geometry against the oracle (same support rule)
+    sub = _subset(m, torch.arange(0, 50_000, 250, device=dev))
+    hs, _ = render_forward(*_params(sub), geo, make_config(sub, scene, "cuda", "noocl", cutoff=PARITY_CUTOFF))
+    ref, _ = _oracle(sub, scene, idx, "cuda", "noocl", PARITY_CUTOFF)
+    _close(hs[idx.to(dev)], ref, 2e-5, msg="C2 subset hist")
+
+
+def test_c3_full_size_train_step_parity():
+    """C3 (the headline): 100k Gaussians -> 128x128 wall x 1024 bins, cuda preset, cutoff 5.7 sigma,
+    forward recording the ray cache + backward walking it (the bench's path).  Whole volume finite;
+    2 wall points vs the dense HIP evaluation (hist and gradients seeded there); a Gaussian subset vs
+    the oracle."""
+    from nlosgr import GaussianParams
+    from nlosgr.render import render_backward, render_forward
+    from nlosgr.volume import Scene, make_config
+    dev = torch.device("cuda:0")
+    scene = Scene(H=128, W=128, T=1024, ns=32)
+    m = GaussianParams.synthetic(100_000, 3, preset="cuda", device=dev, seed=0)
+    geo = scene.geometry(dev, "cuda", "noocl")
+    cfg = make_config(m, scene, "cuda", "noocl", cutoff=PARITY_CUTOFF)
+    hist, _, ws = render_forward(*_params(m), geo, cfg, ray_cache=True)
+    _finite_volume(hist)
+    idx = torch.tensor([128 * 40 + 30, 128 * 100 + 90], device=dev)
+    g = torch.Generator().manual_seed(3)
+    gseed = torch.randn(len(idx), 1024, generator=g).to(dev)
+    gfull = torch.zeros(128 * 128, 1024, device=dev)
+    gfull[idx] = gseed
+    d = render_backward(*_params(m), geo, cfg, grad_hist=gfull, workspace=ws, ray_cache=True)
+    del ws
+    for t in d:
+        assert torch.isfinite(t).all()
+    _culled_vs_dense(m, scene, "cuda", idx, hist, d, gseed)
+    sub = _subset(m, torch.arange(0, 100_000, 1000, device=dev))
+    hs, _ = render_forward(*_params(sub), geo, make_config(sub, scene, "cuda", "noocl", cutoff=PARITY_CUTOFF))
+    ref, _ = _oracle(sub, scene, idx.cpu(), "cuda", "noocl", PARITY_CUTOFF)
+    _close(hs[idx], ref, 2e-5, msg="C3 subset hist")
+
+
+def test_c4_full_size_binint_vs_numerical():
+    """C4: the bin-integrated (analytic) forward vs the numerical one on the C3 inputs, whole volume:
+    the two integrate the same pdf, one per bin-average and one per bin-centre sample, so they
+    agree to the curvature term (rel-L2 5e-5 measured at 3 sigma in round 1)."""
+    from nlosgr import GaussianParams
+    from nlosgr.render import render_forward
+    from nlosgr.volume import Scene, make_config
+    dev = torch.device("cuda:0")
+    scene = Scene(H=128, W=128, T=1024, ns=32)
+    m = GaussianParams.synthetic(100_000, 3, preset="cuda", device=dev, seed=0)
+    h_num, _ = render_forward(*_params(m), scene.geometry(dev, "cuda", "noocl"),
+                              make_config(m, scene, "cuda", "noocl", cutoff=PARITY_CUTOFF))
+    h_int, _ = render_forward(*_params(m), scene.geometry(dev, "cuda", "binint"),
+                              make_config(m, scene, "cuda", "binint", cutoff=PARITY_CUTOFF))
+    _finite_volume(h_int)
+    rel = float((h_int - h_num).norm() / h_num.norm())
+    assert rel < 1e-3, f"binint vs numerical rel-L2 {rel:.3e}"
+
+
+def test_c5_band_full_size():
+    """C5 (500k Gaussians -> 256x256 wall x 2048 bins) is an 8-GPU config: one rank's band (1/8 of
+    the wall) at full size, forward at 5.7 sigma, finite; one wall point vs the dense HIP evaluation;
+    a Gaussian subset vs the oracle on 1 wall point."""
+    from nlosgr import GaussianParams
+    from nlosgr.distributed import wall_band
+    from nlosgr.render import render_forward
+    from nlosgr.volume import Scene, make_config
+    dev = torch.device("cuda:0")
+    scene = Scene(H=256, W=256, T=2048, ns=32)
+    m = GaussianParams.synthetic(500_000, 3, preset="cuda", device=dev, seed=0)
+    b0, b1 = wall_band(256 * 256, 3, 8)
+    walls = scene.walls(dev)[b0:b1].contiguous()
+    geo = scene.geometry(dev, "cuda", "noocl", walls=walls)
+    cfg = make_config(m, scene, "cuda", "noocl", cutoff=PARITY_CUTOFF)
+    hist, _ = render_forward(*_params(m), geo, cfg)
+    assert hist.shape == (b1 - b0, 2048)
+    _finite_volume(hist)
+    k = 4000
+    gdense = scene.geometry(dev, "cuda", "noocl", walls=walls[k:k + 1].contiguous())
+    ref, _ = render_forward(*_params(m), gdense, make_config(m, scene, "cuda", "noocl", cutoff=0.0))
+    _close(hist[k:k + 1], ref, 1e-5, msg="C5 band culled vs dense")
+    sub = _subset(m, torch.arange(0, 500_000, 5000, device=dev))
+    hs, _ = render_forward(*_params(sub), gdense, make_config(sub, scene, "cuda", "noocl", cutoff=PARITY_CUTOFF))
+    ref, _ = _oracle(sub, scene, torch.tensor([b0 + k]), "cuda", "noocl", PARITY_CUTOFF)
+    _close(hs, ref, 2e-5, msg="C5 subset hist")

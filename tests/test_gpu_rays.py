@@ -49,18 +49,40 @@ def _oracle(m, deg):
                     cpu(m._features_rest), deg), cpu(feats)
 
 
-@pytest.mark.parametrize("ng,shift", [(200, 0.5), (400, 3.0)])
+@pytest.mark.parametrize("preset", ["cuda", "torch"])
+def test_bboxes_match_oracle(preset):
+    """nlosgr_bboxes vs the restated compute_gaussian_bboxes_kernel (bbox_compute.cuh:23-120, cuda)
+    and GaussianModel.get_bboxes (gaussian_model.py:140-178, torch), incl. a zero quaternion (cuda:
+    identity) and sigma 2.5 / modifier 0.8.  fp32 ops in a different association: 4 ulp of the box."""
+    from nlosgr.render import bboxes
+    from oracle import torch_ref as R
+    m, _, _ = _scene(300, 1, 5, scale_shift=0.3)
+    with torch.no_grad():
+        if preset == "cuda":
+            m._rotation[7].zero_()
+    P, _ = _oracle(m, 0)
+    for mod, sig in ((1.0, 3.0), (0.8, 2.5)):
+        got = bboxes(m._mu, m._scaling, m._rotation, mod, sig, preset=preset).reshape(-1, 6).cpu()
+        ref = (R.bboxes_cuda if preset == "cuda" else R.bboxes_torch)(P, mod, sig)
+        _close(got, ref, 5e-7, 0.0, f"{preset} boxes mod {mod} sigma {sig}")
+        ext = (got[:, 3:] - got[:, :3]) / 2
+        assert torch.all(ext > 0)
+
+
+@pytest.mark.parametrize("ng,shift", [(200, 0.5), (400, 3.0), (2000, 1.0)])
 def test_filter_matches_oracle(ng, shift):
-    from nlosgr.rays import gaussian_filter
+    """Index work is bit-exact: the HIP filter and the oracle's restatement of
+    filter_gaussians_kernel (ray_aabb.cu:10-61, slab test cuda_utils.cuh:97-121) get the SAME boxes
+    and must return identical int32 rows (count, first 256 hits by index, -1 padding)."""
+    from nlosgr.rays import filter_gaussians_per_ray
+    from nlosgr.render import bboxes
     from oracle import torch_ref as R
     m, o, d = _scene(ng, 40, 11, scale_shift=shift)
-    filt = gaussian_filter(o, d, m._mu, m._scaling, m._rotation)
-    P, _ = _oracle(m, 0)
-    ref = R.aabb_filter(o.cpu(), d.cpu(), R.bboxes_cuda(P))
-    got = filt.cpu()
-    # a box face within fp32 rounding of the ray can flip one hit; everything else is exact
-    diff = (got != ref).any(dim=1)
-    assert int(diff.sum()) <= 1, f"{int(diff.sum())} rows differ"
+    bb = bboxes(m._mu, m._scaling, m._rotation, 1.0, 3.0, preset="cuda").reshape(-1, 6)
+    got = filter_gaussians_per_ray(o, d, m._mu, bb).cpu()
+    ref = R.aabb_filter(o.cpu(), d.cpu(), bb.cpu())
+    assert got.dtype == ref.dtype == torch.int32
+    assert torch.equal(got, ref)
     if shift >= 3.0:
         assert torch.all(got[:, 0] == 256)
 
@@ -131,3 +153,42 @@ def test_render_module_dropin():
                               ("rotation", m._rotation, P._rotation), ("opacity", m._opacity, P._opacity),
                               ("features_dc", m._features_dc, P._features_dc)]:
         _close(leaf.grad, rleaf.grad, 2e-4, atol=1e-6, msg=f"grad {name}")
+
+
+@pytest.mark.parametrize("occl", [False, True])
+def test_nlos_gaussian_renderer_dropin(occl):
+    """NLOSGaussianRenderer (submodules/cuda_renderer/__init__.py:24-180): render() against the
+    same computation on the oracle (boxes, filter, render_rays, attenuation, angular sum) and
+    filter_gaussians() bit-exact against the oracle filter fed the same [Ng, 2, 3] boxes."""
+    from nlosgr.cuda_renderer import create_renderer
+    from nlosgr.render import bboxes
+    from oracle import torch_ref as R
+    dev = torch.device("cuda:0")
+    m, _, _ = _scene(80, 1, 41, scale_shift=1.2, opac_shift=2.0 if occl else 0.0, deg=1)
+    cam = torch.tensor([0.05, 0.0, -0.05], device=dev)
+    rend = create_renderer(3.0)
+    tr_, pr_ = (0.4, 1.6), (0.9, 2.3)
+    nt, npp, nr, c, dT = 7, 9, 48, 1.0, (0.3 if occl else 0.03)
+    result, hist = rend.render(m, cam, tr_, pr_, (0.2, 1.4), nt, npp, nr, c, dT, 1.0, occl, "netf")
+    assert result.shape == (nr, nt, npp) and hist.shape == (nr,)
+    assert not result.requires_grad
+    P, _ = _oracle(m, 1)
+    theta = torch.linspace(*tr_, nt)
+    phi = torch.linspace(*pr_, npp)
+    tg, pg = torch.meshgrid(theta, phi, indexing="ij")
+    tf, pf = tg.reshape(-1), pg.reshape(-1)
+    d = torch.stack([torch.sin(tf) * torch.cos(pf), torch.sin(tf) * torch.sin(pf), torch.cos(tf)], 1)
+    o = cam.cpu().unsqueeze(0).expand(tf.shape[0], 3).contiguous()
+    t = torch.linspace(0.2, 1.4, nr)
+    with torch.no_grad():
+        filt = R.aabb_filter(o, d, R.bboxes_cuda(P))
+        # the reference passes features_dc only (__init__.py:112-115): degree 1 reads just the dc term
+        rho, _, _ = R.render_rays_cuda(o, d, t, P, P._features_dc[:, :, 0], cam.cpu(), 0, c, dT, 1.0, occl, filt)
+    ref = rho.T.reshape(nr, nt, npp) / (t.view(-1, 1, 1) ** 2 + 1e-8) * torch.sin(tg.unsqueeze(0))
+    ref_h = ref.sum(dim=(1, 2)) * ((tr_[1] - tr_[0]) / nt) * ((pr_[1] - pr_[0]) / npp)
+    tol = 2e-4 if occl else 2e-5
+    _close(result, ref, tol, msg="result")
+    _close(hist, ref_h, tol, msg="hist")
+    bb = bboxes(m._mu, m._scaling, m._rotation, 1.0, 3.0, preset="cuda")
+    got = rend.filter_gaussians(o.to(dev), d.to(dev), m._mu, bb).cpu()
+    assert torch.equal(got, R.aabb_filter(o, d, bb.reshape(-1, 6).cpu()))
