@@ -23,6 +23,7 @@ every rank a full volume of its own capture (weak scaling).
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config C3] [--cutoff 5.7] [--lines 3.0] [--band 8] [--replicas]
 """
 import argparse
+from dataclasses import replace
 import json
 import os
 import statistics
@@ -199,8 +200,11 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--preset", default="cuda", choices=("cuda", "torch"),
                     help="convention preset: cuda = the reference's CUDA path, torch = its torch path (SURVEY A.3)")
-    ap.add_argument("--mode", default="noocl", choices=("noocl", "netf"),
-                    help="rendering_type: noocl (configs/default.py:15 default) or netf self-transmittance")
+    ap.add_argument("--mode", default="noocl", choices=("noocl", "netf", "occl"),
+                    help="noocl (configs/default.py:15 default), netf self-transmittance, or occl = path C's "
+                         "shared-transmittance compositing (ray-tile engine)")
+    ap.add_argument("--selection", default="support", choices=("support", "aabb"),
+                    help="support = Mahalanobis cutoff; aabb = path C's 3-sigma box filter, 256 per ray")
     ap.add_argument("--band", type=int, default=0,
                     help="single GPU: time EVERY band of a BAND-way wall shard in turn (one rank's share each); "
                          "value = projected job rate 1 / max-over-bands step time (the all-reduce is not timed)")
@@ -245,7 +249,7 @@ def main():
     cutoffs = [a.cutoff] + [float(x) for x in a.lines.split(",") if x.strip()]
     results = {}
     for cut in cutoffs:
-        cfg = make_config(model, scene, a.preset, a.mode, cutoff=cut)
+        cfg = make_config(model, scene, a.preset, a.mode, cutoff=cut, selection=a.selection)
         per_band = []
         for (b0, b1) in bands:
             whole = (b0, b1) == (0, H * W)
@@ -276,7 +280,10 @@ def main():
             snap.restore()
             params = [model._mu.detach(), model._scaling.detach(), model._rotation.detach(),
                       model._opacity.detach(), features_flat(model).detach().contiguous()]
-            pairs, rays, evals = count_support(*params, geo, cfg)
+            if a.selection == "aabb":
+                pairs = rays = evals = None      # no support count for the box filter
+            else:   # occl: the same (pair, ray, bin) support as noocl at this cutoff
+                pairs, rays, evals = count_support(*params, geo, replace(cfg, mode="noocl") if a.mode == "occl" else cfg)
             per_band.append({"band": [b0, b1], "ms_per_step": elapsed * 1000.0 / a.steps,
                              "fwd_ms": statistics.fmean(fwd_ms), "bwd_ms": statistics.fmean(bwd_ms) if bwd_ms else 0.0,
                              "fwd_ms_all": fwd_ms, "bwd_ms_all": bwd_ms, "pairs": pairs, "rays": rays,
@@ -312,9 +319,10 @@ def main():
     # compute-side figures: exact in-support evaluations of the (frozen) workload per second, and the
     # VALU issue utilisation from the committed SQ counter pass of this command
     # (SQ_INSTS_VALU x 2 cycles per wave64 instruction / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs))
-    valu = {"evaluations": worst["evaluations"], "pairs": worst["pairs"], "rays": worst["rays"],
-            "evals_per_s_fwd": worst["evaluations"] / (fwd_avg * 1e-3),
-            "evals_per_s_bwd": worst["evaluations"] / (bwd_avg * 1e-3) if bwd_avg else None}
+    ev = worst["evaluations"]
+    valu = {"evaluations": ev, "pairs": worst["pairs"], "rays": worst["rays"],
+            "evals_per_s_fwd": ev / (fwd_avg * 1e-3) if ev else None,
+            "evals_per_s_bwd": ev / (bwd_avg * 1e-3) if (ev and bwd_avg) else None}
     sq, sq_src = committed_profile(a.config, "valu", a.cutoff) if single else (None, None)
     if sq:
         valu["valu_issue_util"] = sq.get("valu_issue_util")
@@ -328,11 +336,12 @@ def main():
         "scaling": "strong" if sharded else "weak", "vs_baseline": None,
         "dtype": "f32", "data": "synthetic (SURVEY §8d geometry, seeded random Gaussians and target)",
         "config": {"workload": f"{a.config}: {ng} Gaussians -> {H}x{W} wall x {T} bins, {ns}x{ns} angular "
-                               f"samples, {a.preset} preset, {'no occlusion' if a.mode == 'noocl' else a.mode}, "
+                               f"samples, {a.preset} preset, {'no occlusion' if a.mode == 'noocl' else a.mode}"
+                               f"{', path C AABB selection (256 per ray)' if a.selection == 'aabb' else ''}, "
                                f"{'dense (every sample)' if a.cutoff <= 0 else f'support cutoff {a.cutoff} sigma'}, "
                                f"{'fwd' if fwd_only else 'fwd+MSE+bwd (6 param grads)+Adam'}, frozen workload",
                    "gaussians": ng, "wall": [H, W], "bins": T, "angular": ns, "cutoff": a.cutoff,
-                   "preset": a.preset, "mode": a.mode,
+                   "preset": a.preset, "mode": a.mode, "selection": a.selection,
                    "parallelism": (f"wall shard: {world} bands (rank r renders band r), packed grad all-reduce"
                                    if sharded else
                                    f"all {a.band} bands of a {a.band}-way wall shard timed in turn on one GPU "

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define NLOSGR_ABI_VERSION 4
+#define NLOSGR_ABI_VERSION 5
 
 /* convention presets */
 enum {
@@ -50,9 +50,20 @@ enum {
 enum {
     NLOSGR_MODE_NOOCL = 0, /* rho_d = sum_g sigma pdf rho                  (gaussian_model.py:346-364) */
     NLOSGR_MODE_NETF = 1,  /* per-Gaussian self-transmittance cumprod       (gaussian_model.py:313-324) */
-    NLOSGR_MODE_BININT = 2 /* no-occlusion with each sample replaced by the exact average of the pdf
+    NLOSGR_MODE_BININT = 2, /* no-occlusion with each sample replaced by the exact average of the pdf
                               over its radial bin [r_k -+ dr/2] (closed-form erf; forward only) — the
                               corrected counterpart of the analytic section path */
+    NLOSGR_MODE_OCCL = 3   /* path C use_occlusion=True (volume_renderer.cu:80-137), cuda preset only:
+                              per ray, T_k = exp(-c dT sum_{k'<k} D_k'), D = sum_g sigma pdf,
+                              rho_d = T_k sum_g (1 - exp(-sigma pdf c dT)) rho, zero where T_k < 1e-4 */
+};
+
+/* which Gaussians each ray sums over (nlosgr_options.selection) */
+enum {
+    NLOSGR_SELECT_SUPPORT = 0, /* every Gaussian, samples within the Mahalanobis cutoff (dense if <= 0) */
+    NLOSGR_SELECT_AABB = 1     /* path C's filter (ray_aabb.cu:10-61, volume_renderer.cu:220-245): the first
+                                  256 Gaussians by index whose 3-sigma box (bbox_compute.cuh) the ray hits,
+                                  each evaluated along the whole ray; cuda preset only */
 };
 
 enum {
@@ -107,6 +118,9 @@ typedef struct {
                                  see nlosgr_workspace_bytes) and a backward on the SAME workspace with
                                  the SAME inputs walks that record instead of re-testing the rays.
                                  Culled (cutoff > 0), histogram-only calls; 0 = off */
+    int32_t selection;        /* NLOSGR_SELECT_*.  OCCL mode and AABB selection run the ray-tile engine
+                                 (ray-major, per-ray compositing, deterministic); the ray cache and
+                                 nlosgr_count_support do not apply there */
 } nlosgr_options;
 
 /* Scratch bytes needed by fwd/bwd for this problem (caller allocates, 256-B aligned); includes

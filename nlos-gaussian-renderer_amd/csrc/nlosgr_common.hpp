@@ -100,6 +100,37 @@ inline void launch_preprocess(const nlosgr_gaussians* g, GaussRec* recs, hipStre
         hipLaunchKernelGGL(preprocess_kernel<NLOSGR_PRESET_CUDA>, dim3(nb), dim3(kBlock), 0, s, *g, recs);
 }
 
+// sig-sigma axis-aligned box of Gaussian i: bbox_compute.cuh:23-71 (cuda: s = exp(S) mod, identity for a
+// zero quaternion) / gaussian_model.py:140-178 (torch: F.normalize then build_rotation, clamp 1e-8).
+// out = (min xyz, max xyz)
+template <int PRESET>
+__device__ __forceinline__ void gauss_bbox(const nlosgr_gaussians& g, int i, float sig, float* out) {
+    float s[3];
+    for (int t = 0; t < 3; ++t) s[t] = expf(g.scaling[3 * i + t]) * g.scaling_modifier;
+    const float* Q = g.rotation + 4 * i;
+    float n = sqrtf(Q[0] * Q[0] + Q[1] * Q[1] + Q[2] * Q[2] + Q[3] * Q[3]);
+    float R[9];
+    if (PRESET == NLOSGR_PRESET_CUDA && n < 1e-8f) {
+        R[0] = 1.f; R[1] = 0.f; R[2] = 0.f; R[3] = 0.f; R[4] = 1.f; R[5] = 0.f; R[6] = 0.f; R[7] = 0.f; R[8] = 1.f;
+    } else {
+        if (PRESET == NLOSGR_PRESET_TORCH) n = fmaxf(n, 1e-12f);
+        float q[4] = {Q[0] / n, Q[1] / n, Q[2] / n, Q[3] / n};
+        if (PRESET == NLOSGR_PRESET_TORCH) {
+            const float n1 = sqrtf(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+            for (int t = 0; t < 4; ++t) q[t] /= n1;
+        }
+        quat_rot(q[0], q[1], q[2], q[3], R);
+    }
+    for (int r = 0; r < 3; ++r) {
+        float v = 0.f;
+        for (int c = 0; c < 3; ++c) v += (R[3 * r + c] * s[c]) * (R[3 * r + c] * s[c]);
+        if (PRESET == NLOSGR_PRESET_TORCH) v = fmaxf(v, 1e-8f);
+        const float e = sig * sqrtf(v);
+        out[r] = g.mu[3 * i + r] - e;
+        out[3 + r] = g.mu[3 * i + r] + e;
+    }
+}
+
 // dL/dA (acc[0..8], A = diag(1/s~) R') -> dL/d_scaling, dL/d_rotation of Gaussian i under the preset
 template <int PRESET>
 __device__ void chain_to_raw(const nlosgr_gaussians& g, int i, const float* acc, float* d_scaling, float* d_rot) {
@@ -160,6 +191,16 @@ __device__ void chain_to_raw(const nlosgr_gaussians& g, int i, const float* acc,
         }
     }
 }
+
+// ray-tile engine (nlosgr_tiles.hip): NLOSGR_MODE_OCCL and NLOSGR_SELECT_AABB
+bool tiles_engine(const nlosgr_options* opt);
+int tiles_validate(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_options* opt);
+size_t tiles_workspace_bytes(const nlosgr_gaussians* g, const nlosgr_geometry* geo);
+int tiles_fwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_options* opt, void* ws,
+              float* hist_out, float* ray_out, hipStream_t s);
+int tiles_bwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_options* opt, void* ws,
+              const float* grad_hist, const float* grad_ray, float* d_mu, float* d_scaling, float* d_rotation,
+              float* d_opacity, float* d_features, hipStream_t s);
 
 }  // namespace detail
 }  // namespace nlosgr

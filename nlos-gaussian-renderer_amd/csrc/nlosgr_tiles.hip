@@ -1,0 +1,841 @@
+// Ray-tile engine (gfx950): per-ray compositing over the batched spherical geometry.
+//
+// It serves the two path C semantics the pair-major kernels of nlosgr_volume.hip cannot express,
+// because both make a sample's value depend on the other Gaussians of the same ray:
+//   * NLOSGR_MODE_OCCL — shared transmittance (volume_renderer.cu:80-137): per ray,
+//       D_k = sum_g sigma_g pdf_g(x_k),  W_k = sum_g rho_g (1 - exp(-sigma_g pdf_g(x_k) c dT)),
+//       T_k = exp(-c dT sum_{k'<k} D_k'),  out_k = T_k W_k, and 0 from the first T_k < 1e-4 on;
+//   * NLOSGR_SELECT_AABB — path C's filter (ray_aabb.cu:10-61 + volume_renderer.cu:220-245): a ray
+//       sums only the first 256 Gaussians, by index, whose 3-sigma box (bbox_compute.cuh) it hits,
+//       each over the whole ray (bins with m^2 <= kFullM2; beyond, pdf < 1e-39 underflows anyway).
+// With NLOSGR_SELECT_SUPPORT a ray sums every Gaussian over the bins within the Mahalanobis cutoff
+// (dense when cutoff <= 0), as the pair-major kernels do.
+//
+// Work item = (wall point p, ray tile t): a TI x TJ block of the (theta, phi) ray grid, sized so
+// the tile's [ray][bin] float2 rows fill 128 KB of LDS.  Persistent grid, one 8-wave workgroup per
+// CU; slot s takes items s, s + nslot, ... (a static schedule, so every sum has a fixed order).
+//   cull  : the 8 waves test 512 Gaussians per round (lane = Gaussian) against the tile's cone with
+//           the bounding sphere of the support (or of the box); passing indices queue in LDS in
+//           index order.
+//   stage : 128 queued Gaussians at a time become pair records in LDS (A, u0 = A(p - mu), quadric
+//           or box, sigma, rho = SH albedo of the view direction mu - p).
+//   rays  : wave = ray.  Lane = staged Gaussian runs the ray test (quadric / slab + the 256 cap in
+//           index order) and forms its 1-D Gaussian along the ray; then lane = bin: each 64-bin chunk
+//           takes the entries overlapping it (ballot, in index order) and adds D and W into the
+//           tile's rows (every lane owns its bin: no conflicts, no atomics).
+//   scan  : wave = ray, lane = bin: exclusive wave scan of c dT D -> T, liveness, out = T W.
+//           forward : sin(theta) out rows summed over the tile in row order -> partial histogram
+//                     [p][t][nr]; tiles_reduce_kernel sums the tiles in order (x att x hscale).
+//           backward: rows become (a, b) = (dL/dW, dL/dD), b from a suffix scan.
+//   pairs : (backward) lane = (staged Gaussian, ray group) walks the in-support bins of its rays
+//           reading (a, b) and accumulates the moments of dL/dpdf pdf; the four ray groups combine
+//           in LDS in a fixed order; one 32-float record per (item, Gaussian) is added into the
+//           slot's private accumulator row (plain read-modify-write).
+//   finish: sums each Gaussian's slot rows in slot order and chains to the raw parameters.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <string.h>
+
+#include "nlosgr_common.hpp"
+
+using namespace nlosgr;
+using namespace nlosgr::detail;
+
+namespace {
+
+constexpr int kTB = 512;               // threads per workgroup (8 waves)
+constexpr int kTW = kTB / 64;
+constexpr int kWin = 128;              // staged Gaussians per window
+constexpr int kQCap = kTB + kWin;      // queue capacity (indices)
+constexpr int kStage = 20;             // floats per staged pair: A[9] u0[3] sel[6] sigma rho
+constexpr int kRec = 32;               // floats per accumulator row: dA[9] dmu[3] dsigma pad[3] dF[16]
+constexpr int kCap = NLOSGR_MAX_PER_RAY;
+constexpr float kFullM2 = 180.0f;      // AABB selection: whole-ray support, pdf >= exp(-90)
+constexpr float kLog2e = 1.44269504088896341f;
+constexpr int kRowFloats = 32768;      // [ray][bin] float2 rows: 128 KB
+
+struct TArgs {
+    nlosgr_gaussians g;
+    nlosgr_geometry geo;
+    nlosgr_options opt;
+    const GaussRec* recs;
+    const float4* cull;      // [ng] (mu, bounding-sphere radius of the support / box)
+    const float* bbox;       // [ng][6] (AABB selection)
+    float* acc;              // [nslot][ng][kRec] (backward)
+    float* hpart;            // [P][ntiles][nr] (forward)
+    float* hist_out;
+    float* ray_out;
+    const float* grad_hist;
+    const float* grad_ray;
+    int ti, tj, rt;          // tile shape and rays per tile
+    int ntile_i, ntile_j, ntiles;
+    long long nitems;
+    int nslot;
+};
+
+__host__ __device__ inline int tile_rays(int nr) {
+    int rt = 64;
+    while (rt > 4 && 2 * rt * nr > kRowFloats) rt >>= 1;
+    return rt;
+}
+
+struct TLayout {   // offsets in floats
+    int rows, stage, queue, comb, misc, total;
+    __host__ __device__ TLayout(int rt, int nr) {
+        rows = 0;
+        stage = rows + 2 * rt * nr;
+        queue = stage + kWin * kStage;
+        comb = queue + kQCap;
+        misc = comb + kWin * 16;
+        total = misc + 256;
+    }
+};
+
+__device__ __forceinline__ float quadric(const float* M, float dx, float dy, float dz) {
+    const float t0 = fmaf(M[0], dx, fmaf(M[1], dy, M[2] * dz));
+    const float t1 = fmaf(M[3], dy, M[4] * dz);
+    return fmaf(dx, t0, fmaf(dy, t1, dz * dz * M[5]));
+}
+
+// value of lane s (wave-uniform s) as a scalar
+__device__ __forceinline__ float rlf(float v, int s) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), s));
+}
+__device__ __forceinline__ int rli(int v, int s) { return __builtin_amdgcn_readlane(v, s); }
+
+// SH albedo term sh = f . Y(dir) over the active coefficients
+__device__ __forceinline__ float sh_dot(const float* f, const float* Y, int K) {
+    float sh = 0.f;
+#pragma unroll
+    for (int c = 0; c < kMaxK; ++c)
+        if (c < K) sh += f[c] * Y[c];
+    return sh;
+}
+
+__device__ __forceinline__ float wave_incl_sum(float x) {
+    const int lane = lane_id();
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const float u = __shfl_up(x, off);
+        if (lane >= off) x += u;
+    }
+    return x;
+}
+
+__device__ __forceinline__ float wave_incl_suffix(float x) {
+    const int lane = lane_id();
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const float u = __shfl_down(x, off);
+        if (lane + off < 64) x += u;
+    }
+    return x;
+}
+
+__device__ __forceinline__ int wave_min_i(int x) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) x = min(x, __shfl_xor(x, off));
+    return x;
+}
+
+__device__ __forceinline__ int wave_max_i(int x) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) x = max(x, __shfl_xor(x, off));
+    return x;
+}
+
+// slab test of the half-infinite ray o + t d against a box (cuda_utils.cuh:97-121, IEEE ops)
+__device__ __forceinline__ bool slab_hit(const float* bb, float ox, float oy, float oz, float ix, float iy, float iz) {
+    const float tx0 = (bb[0] - ox) * ix, tx1 = (bb[3] - ox) * ix;
+    const float ty0 = (bb[1] - oy) * iy, ty1 = (bb[4] - oy) * iy;
+    const float tz0 = (bb[2] - oz) * iz, tz1 = (bb[5] - oz) * iz;
+    const float tmin = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fminf(tz0, tz1));
+    const float tmax = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
+    return tmax >= tmin && tmax >= 0.0f;
+}
+
+// per-Gaussian cull record: mu and the radius of a sphere containing the support / the box
+template <int SEL>
+__global__ __launch_bounds__(256) void cull_prep_kernel(nlosgr_gaussians g, const GaussRec* recs, float mc,
+                                                        float4* cull, float* bbox) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= g.ng) return;
+    const GaussRec r = recs[i];
+    float rad;
+    if (SEL == NLOSGR_SELECT_AABB) {
+        float b[6];
+        gauss_bbox<NLOSGR_PRESET_CUDA>(g, i, 3.0f, b);
+        for (int t = 0; t < 6; ++t) bbox[6 * (size_t)i + t] = b[t];
+        const float ex = 0.5f * (b[3] - b[0]), ey = 0.5f * (b[4] - b[1]), ez = 0.5f * (b[5] - b[2]);
+        const float cx = 0.5f * (b[3] + b[0]), cy = 0.5f * (b[4] + b[1]), cz = 0.5f * (b[5] + b[2]);
+        // sphere around mu holding the whole box (the box is centred on mu up to rounding)
+        const float off = sqrtf((cx - r.a.x) * (cx - r.a.x) + (cy - r.a.y) * (cy - r.a.y) + (cz - r.a.z) * (cz - r.a.z));
+        rad = (sqrtf(ex * ex + ey * ey + ez * ez) + off) * 1.0001f + 1e-7f;
+    } else {
+        rad = mc > 0.f ? mc * r.d.y * 1.0001f + 1e-7f : INFINITY;
+    }
+    cull[i] = make_float4(r.a.x, r.a.y, r.a.z, rad);
+}
+
+// ------------------------------------------------------------------------------------------
+// the tile kernel (forward: BWD = false; backward: BWD = true)
+// ------------------------------------------------------------------------------------------
+template <int SEL, bool DENSE, bool OCCL, bool BWD>
+__global__ __launch_bounds__(kTB) void tile_kernel(TArgs k) {
+    extern __shared__ __align__(16) float sm[];
+    const int nr = k.geo.nr, nt = k.geo.nt, np_ = k.geo.np;
+    const TLayout L(k.rt, nr);
+    float2* rows = reinterpret_cast<float2*>(sm + L.rows);
+    float* stage = sm + L.stage;
+    int* queue = reinterpret_cast<int*>(sm + L.queue);
+    float* comb = sm + L.comb;
+    float* misc = sm + L.misc;
+    int* icnt = reinterpret_cast<int*>(misc);          // [64] AABB cap counters per ray
+    int* ihalf = icnt + 64;                             // [64] per-window hits of the first staged half
+    int* iwave = icnt + 128;                            // [8] cull counts per wave
+    float* cone = misc + 144;                           // axis xyz, cos h, sin h, pass-all flag
+    const int tid = threadIdx.x, wave = tid >> 6, lane = lane_id();
+    const int RT = k.rt;
+    const float mc2 = SEL == NLOSGR_SELECT_AABB ? kFullM2 : k.opt.cutoff * k.opt.cutoff;
+    const float r0 = k.geo.r[0];
+    const float dr = nr > 1 ? (k.geo.r[nr - 1] - r0) / (float)(nr - 1) : 1.0f;
+    const float inv_dr = 1.0f / dr;
+    const float cdt = k.opt.c_deltaT;
+    const int nch = (nr + 63) / 64;
+    const int deg = k.g.sh_degree, K = (deg + 1) * (deg + 1);
+
+    for (long long item = blockIdx.x; item < k.nitems; item += k.nslot) {
+        const int p = (int)(item / k.ntiles);
+        const int t = (int)(item - (long long)p * k.ntiles);
+        const int ti0 = (t / k.ntile_j) * k.ti, tj0 = (t % k.ntile_j) * k.tj;
+        const float px = k.geo.wall[3 * p], py = k.geo.wall[3 * p + 1], pz = k.geo.wall[3 * p + 2];
+        const float* sth = k.geo.sin_theta + (size_t)p * nt;
+        const float* cth = k.geo.cos_theta + (size_t)p * nt;
+        const float* sph = k.geo.sin_phi + (size_t)p * np_;
+        const float* cph = k.geo.cos_phi + (size_t)p * np_;
+        __syncthreads();   // previous item done with LDS
+        // tile cone (wave 0, lane = ray of the tile)
+        if (wave == 0) {
+            const int i = ti0 + lane / k.tj, j = tj0 + lane % k.tj;
+            const bool v = lane < RT && i < nt && j < np_;
+            float dx = 0.f, dy = 0.f, dz = 0.f;
+            if (v) { dx = sth[i] * cph[j]; dy = sth[i] * sph[j]; dz = cth[i]; }
+            float sx = dx, sy = dy, sz = dz;
+            for (int off = 32; off > 0; off >>= 1) {
+                sx += __shfl_xor(sx, off); sy += __shfl_xor(sy, off); sz += __shfl_xor(sz, off);
+            }
+            const float n = sqrtf(sx * sx + sy * sy + sz * sz);
+            const float ax = n > 0.f ? sx / n : 0.f, ay = n > 0.f ? sy / n : 0.f, az = n > 0.f ? sz / n : 1.f;
+            float c = v ? fminf(1.0f, dx * ax + dy * ay + dz * az) : 1.0f;
+            for (int off = 32; off > 0; off >>= 1) c = fminf(c, __shfl_xor(c, off));
+            const float h = acosf(c) + 2e-4f;
+            if (lane == 0) {
+                cone[0] = ax; cone[1] = ay; cone[2] = az;
+                cone[3] = cosf(h); cone[4] = sinf(h);
+                cone[5] = (h > 1.5f || n == 0.f) ? 1.f : 0.f;
+            }
+            if (lane < 64) icnt[lane] = 0;
+        }
+        for (int x = tid; x < RT * nr; x += kTB) rows[x] = make_float2(0.f, 0.f);
+        __syncthreads();
+        const float ax = cone[0], ay = cone[1], az = cone[2], ch = cone[3], shh = cone[4];
+        const bool pass_all = cone[5] != 0.f;
+
+        // ---------------- sweeps over the Gaussians (forward: 1; backward: 2) ----------------
+        for (int sweep = 0; sweep < (BWD ? 2 : 1); ++sweep) {
+            const bool pairs = BWD && sweep == 1;
+            if (pairs) {
+                // the scan turned the rows into (a, b); reset the cap counters for the replay
+                if (tid < 64) icnt[tid] = 0;
+                __syncthreads();
+            }
+            int qn = 0;
+            for (int g0 = 0; g0 < k.g.ng || qn > 0; g0 += kTB) {
+                // ---- cull round: lane = Gaussian, 512 per round, ordered append ----
+                if (g0 < k.g.ng) {
+                    const int gi = g0 + tid;
+                    bool hit = false;
+                    if (gi < k.g.ng) {
+                        const float4 c = k.cull[gi];
+                        const float vx = c.x - px, vy = c.y - py, vz = c.z - pz;
+                        const float d2 = vx * vx + vy * vy + vz * vz;
+                        const float R2 = c.w * c.w;
+                        if (pass_all || d2 <= R2 || !(c.w < INFINITY)) {
+                            hit = true;
+                        } else {
+                            // angle(v, axis) <= h + asin(R / |v|)  <=>  v.a >= cos h sqrt(|v|^2 - R^2) - sin h R
+                            hit = vx * ax + vy * ay + vz * az >= ch * sqrtf(d2 - R2) - shh * c.w;
+                        }
+                    }
+                    const unsigned long long m = __builtin_amdgcn_ballot_w64(hit);
+                    if (lane == 0) iwave[wave] = __popcll(m);
+                    __syncthreads();
+                    int base = qn;
+                    for (int w = 0; w < wave; ++w) base += iwave[w];
+                    if (hit) queue[base + lanes_below(m)] = gi;
+                    int tot = 0;
+                    for (int w = 0; w < kTW; ++w) tot += iwave[w];
+                    qn += tot;
+                    __syncthreads();
+                }
+                const bool last = g0 + kTB >= k.g.ng;
+                // ---- windows of up to 128 staged Gaussians ----
+                while (qn >= kWin || (last && qn > 0)) {
+                    const int nst = min(qn, kWin);
+                    if (tid < nst) {
+                        const int gi = queue[tid];
+                        const GaussRec rec = k.recs[gi];
+                        float* o = stage + tid * kStage;
+                        const float A[9] = {rec.b.x, rec.b.y, rec.b.z, rec.b.w, rec.c.x, rec.c.y, rec.c.z, rec.c.w, rec.d.x};
+                        const float q0 = px - rec.a.x, q1 = py - rec.a.y, q2 = pz - rec.a.z;
+                        float u0[3];
+                        for (int r = 0; r < 3; ++r) u0[r] = A[3 * r] * q0 + A[3 * r + 1] * q1 + A[3 * r + 2] * q2;
+                        for (int x = 0; x < 9; ++x) o[x] = A[x];
+                        o[9] = u0[0]; o[10] = u0[1]; o[11] = u0[2];
+                        if (SEL == NLOSGR_SELECT_AABB) {
+                            for (int x = 0; x < 6; ++x) o[12 + x] = k.bbox[6 * (size_t)gi + x];
+                        } else if (!DENSE) {
+                            const float N[6] = {rec.d.z, rec.d.w, rec.e.x, rec.e.y, rec.e.z, rec.e.w};
+                            const float wv0 = A[0] * u0[0] + A[3] * u0[1] + A[6] * u0[2];
+                            const float wv1 = A[1] * u0[0] + A[4] * u0[1] + A[7] * u0[2];
+                            const float wv2 = A[2] * u0[0] + A[5] * u0[1] + A[8] * u0[2];
+                            const float kap = u0[0] * u0[0] + u0[1] * u0[1] + u0[2] * u0[2] - mc2;
+                            o[12] = wv0 * wv0 - kap * N[0];
+                            o[13] = 2.0f * (wv0 * wv1 - kap * N[1]);
+                            o[14] = 2.0f * (wv0 * wv2 - kap * N[2]);
+                            o[15] = wv1 * wv1 - kap * N[3];
+                            o[16] = 2.0f * (wv1 * wv2 - kap * N[4]);
+                            o[17] = wv2 * wv2 - kap * N[5];
+                        }
+                        o[18] = rec.a.w;
+                        // rho = max(0, 0.5 + SH(dir(mu - p))) (volume_renderer.cu:109-111)
+                        float dx, dy, dz, nrm;
+                        view_dir<NLOSGR_PRESET_CUDA>(-q0, -q1, -q2, dx, dy, dz, nrm);
+                        float Y[kMaxK];
+                        sh_basis<NLOSGR_PRESET_CUDA>(deg, dx, dy, dz, Y);
+                        const float sh = sh_dot(k.g.features + (size_t)gi * k.g.k_feat, Y, K);
+                        o[19] = fmaxf(sh + 0.5f, 0.0f);
+                    }
+                    __syncthreads();
+                    if (!pairs) {
+                        // ---- rays: wave = ray, lane = staged entry, then lane = bin ----
+                        for (int r = wave; r < RT; r += kTW) {
+                            const int i = ti0 + r / k.tj, j = tj0 + r % k.tj;
+                            if (i >= nt || j >= np_) continue;
+                            const float dx = sth[i] * cph[j], dy = sth[i] * sph[j], dz = cth[i];
+                            const float ix = 1.0f / (dx + 1e-8f), iy = 1.0f / (dy + 1e-8f), iz = 1.0f / (dz + 1e-8f);
+                            for (int e0 = 0; e0 < nst; e0 += 64) {
+                                const int e = e0 + lane;
+                                const bool valid = e < nst;
+                                const float* o = stage + (valid ? e : 0) * kStage;
+                                bool sel = valid;
+                                if (SEL == NLOSGR_SELECT_AABB) {
+                                    sel = valid && slab_hit(o + 12, px, py, pz, ix, iy, iz);
+                                    const unsigned long long m = __builtin_amdgcn_ballot_w64(sel);
+                                    const int c0 = icnt[r];
+                                    sel = sel && c0 + lanes_below(m) < kCap;
+                                    wave_sync();
+                                    if (lane == 0) icnt[r] = min(kCap, c0 + __popcll(m));
+                                    wave_sync();
+                                } else if (!DENSE && valid) {
+                                    sel = quadric(o + 12, dx, dy, dz) >= 0.f;
+                                }
+                                float ks = 0.f, ga = 0.f, al = -INFINITY, sg = 0.f, rho = 0.f;
+                                int kl = nr, kh = -1;
+                                if (sel) {
+                                    float v[3];
+                                    for (int x = 0; x < 3; ++x) v[x] = o[3 * x] * dx + o[3 * x + 1] * dy + o[3 * x + 2] * dz;
+                                    const float a = v[0] * v[0] + v[1] * v[1] + v[2] * v[2];
+                                    const float b = o[9] * v[0] + o[10] * v[1] + o[11] * v[2];
+                                    const float ia = 1.0f / a;
+                                    const float ts = -b * ia;
+                                    const float z0 = o[9] + ts * v[0], z1 = o[10] + ts * v[1], z2 = o[11] + ts * v[2];
+                                    const float m2min = z0 * z0 + z1 * z1 + z2 * z2;
+                                    ks = (ts - r0) * inv_dr;
+                                    if (DENSE) {
+                                        kl = 0; kh = nr - 1;
+                                    } else if (m2min <= mc2) {
+                                        const float hk = sqrtf((mc2 - m2min) * ia) * inv_dr;
+                                        kl = fidx(ceilf(ks - hk), 0, nr);
+                                        kh = fidx(floorf(ks + hk), -1, nr - 1);
+                                    }
+                                    ga = -0.5f * kLog2e * a * dr * dr;
+                                    al = -0.5f * kLog2e * m2min;
+                                    sg = o[18];
+                                    rho = o[19];
+                                }
+                                const bool live = kl <= kh;
+                                const int lo = wave_min_i(live ? kl : nr);
+                                const int hi = wave_max_i(live ? kh : -1);
+                                if (lo > hi) continue;
+                                for (int c = lo >> 6; c <= (hi >> 6); ++c) {
+                                    unsigned long long cm =
+                                        __builtin_amdgcn_ballot_w64(live && kl <= c * 64 + 63 && kh >= c * 64);
+                                    if (!cm) continue;
+                                    const int kb = c * 64 + lane;
+                                    const float kf = (float)kb;
+                                    float accD = 0.f, accW = 0.f;
+                                    while (cm) {
+                                        const int s = __builtin_ctzll(cm);
+                                        cm &= cm - 1;
+                                        const float sks = rlf(ks, s), sga = rlf(ga, s), sal = rlf(al, s);
+                                        const float ssg = rlf(sg, s), srho = rlf(rho, s);
+                                        const int skl = rli(kl, s), skh = rli(kh, s);
+                                        const float tt = kf - sks;
+                                        const float pdf = fast_exp2(fmaf(sga, tt * tt, sal));
+                                        const float cv = (kb >= skl && kb <= skh) ? ssg * pdf : 0.f;
+                                        if (OCCL) {
+                                            accD += cv;
+                                            accW = fmaf(srho, 1.0f - fast_exp2(-cv * cdt * kLog2e), accW);
+                                        } else {
+                                            accW = fmaf(srho, cv, accW);
+                                        }
+                                    }
+                                    if (kb < nr) {
+                                        float2 v = rows[r * nr + kb];
+                                        v.x += accD;
+                                        v.y += accW;
+                                        rows[r * nr + kb] = v;
+                                    }
+                                }
+                            }
+                        }
+                    } else {
+                        // ---- pairs (backward): lane = (staged entry, ray group) ----
+                        const int half = wave & 1, rg = wave >> 1;
+                        const int e = half * 64 + lane;
+                        const bool valid = e < nst;
+                        const float* o = stage + (valid ? e : 0) * kStage;
+                        float A[9], u0[3], sel6[6];
+                        for (int x = 0; x < 9; ++x) A[x] = o[x];
+                        for (int x = 0; x < 3; ++x) u0[x] = o[9 + x];
+                        for (int x = 0; x < 6; ++x) sel6[x] = o[12 + x];
+                        const float sg = o[18], rho = o[19];
+                        if (SEL == NLOSGR_SELECT_AABB) {
+                            // hits of the first staged half per ray (the second half's cap ranks follow them)
+                            if (half == 0)
+                                for (int r = rg; r < RT; r += 4) {
+                                    const int i = ti0 + r / k.tj, j = tj0 + r % k.tj;
+                                    bool h = false;
+                                    if (valid && i < nt && j < np_) {
+                                        const float dx = sth[i] * cph[j], dy = sth[i] * sph[j], dz = cth[i];
+                                        h = slab_hit(sel6, px, py, pz, 1.0f / (dx + 1e-8f), 1.0f / (dy + 1e-8f),
+                                                     1.0f / (dz + 1e-8f));
+                                    }
+                                    const unsigned long long m = __builtin_amdgcn_ballot_w64(h);
+                                    if (lane == 0) ihalf[r] = __popcll(m);
+                                }
+                            __syncthreads();
+                        }
+                        float dA[9] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+                        float gU[3] = {0.f, 0.f, 0.f};
+                        float dsig = 0.f, drho = 0.f;
+                        for (int r = rg; r < RT; r += 4) {
+                            const int i = ti0 + r / k.tj, j = tj0 + r % k.tj;
+                            if (i >= nt || j >= np_) continue;
+                            const float dx = sth[i] * cph[j], dy = sth[i] * sph[j], dz = cth[i];
+                            bool sel = valid;
+                            if (SEL == NLOSGR_SELECT_AABB) {
+                                sel = valid && slab_hit(sel6, px, py, pz, 1.0f / (dx + 1e-8f), 1.0f / (dy + 1e-8f),
+                                                        1.0f / (dz + 1e-8f));
+                                const unsigned long long m = __builtin_amdgcn_ballot_w64(sel);
+                                const int rank = icnt[r] + (half ? ihalf[r] : 0) + lanes_below(m);
+                                sel = sel && rank < kCap;
+                            } else if (!DENSE && valid) {
+                                sel = quadric(sel6, dx, dy, dz) >= 0.f;
+                            }
+                            if (!sel) continue;
+                            float v[3];
+                            for (int x = 0; x < 3; ++x) v[x] = A[3 * x] * dx + A[3 * x + 1] * dy + A[3 * x + 2] * dz;
+                            const float a = v[0] * v[0] + v[1] * v[1] + v[2] * v[2];
+                            const float b = u0[0] * v[0] + u0[1] * v[1] + u0[2] * v[2];
+                            const float ia = 1.0f / a;
+                            const float ts = -b * ia;
+                            const float zs[3] = {u0[0] + ts * v[0], u0[1] + ts * v[1], u0[2] + ts * v[2]};
+                            const float m2min = zs[0] * zs[0] + zs[1] * zs[1] + zs[2] * zs[2];
+                            const float ks = (ts - r0) * inv_dr;
+                            int kl = 0, kh = nr - 1;
+                            if (!DENSE) {
+                                if (!(m2min <= mc2)) continue;
+                                const float hk = sqrtf((mc2 - m2min) * ia) * inv_dr;
+                                kl = fidx(ceilf(ks - hk), 0, nr);
+                                kh = fidx(floorf(ks + hk), -1, nr - 1);
+                            }
+                            const float ga = -0.5f * kLog2e * a * dr * dr;
+                            const float al = -0.5f * kLog2e * m2min;
+                            float m0 = 0.f, m1 = 0.f, m2 = 0.f;
+                            const float2* row = rows + r * nr;
+                            for (int kb = kl; kb <= kh; ++kb) {
+                                const float tt = (float)kb - ks;
+                                const float pdf = fast_exp2(fmaf(ga, tt * tt, al));
+                                const float cv = sg * pdf;
+                                const float2 ab = row[kb];
+                                float dc;
+                                if (OCCL) {
+                                    const float ex = fast_exp2(-cv * cdt * kLog2e);
+                                    dc = fmaf(ab.x * rho * cdt, ex, ab.y);
+                                    drho = fmaf(ab.x, 1.0f - ex, drho);
+                                } else {
+                                    dc = ab.x * rho;
+                                    drho = fmaf(ab.x, cv, drho);
+                                }
+                                dsig = fmaf(dc, pdf, dsig);
+                                const float G = dc * cv;
+                                m0 += G;
+                                m1 = fmaf(G, tt, m1);
+                                m2 = fmaf(G * tt, tt, m2);
+                            }
+                            // pdf = exp(-|z|^2 / 2), z_k = zs + tau_k v, tau = (k - ks) dr:
+                            // dL/du0 = -(zs M0 + v M1), dL/dv = -(zs (M1 + ts M0) + v (M2 + ts M1))
+                            const float M0 = m0, M1 = m1 * dr, M2 = m2 * dr * dr;
+                            const float d3[3] = {dx, dy, dz};
+                            for (int x = 0; x < 3; ++x) {
+                                const float gu = -(zs[x] * M0 + v[x] * M1);
+                                const float gv = -(zs[x] * (M1 + ts * M0) + v[x] * (M2 + ts * M1));
+                                gU[x] += gu;
+                                for (int c = 0; c < 3; ++c) dA[3 * x + c] = fmaf(gv, d3[c], dA[3 * x + c]);
+                            }
+                        }
+                        // combine the four ray groups per entry in order rg = 0..3
+                        for (int step = 0; step < 4; ++step) {
+                            if (rg == step && valid) {
+                                float* cb = comb + e * 16;
+                                if (step == 0) {
+                                    for (int x = 0; x < 9; ++x) cb[x] = dA[x];
+                                    cb[9] = gU[0]; cb[10] = gU[1]; cb[11] = gU[2]; cb[12] = dsig; cb[13] = drho;
+                                } else {
+                                    for (int x = 0; x < 9; ++x) cb[x] += dA[x];
+                                    cb[9] += gU[0]; cb[10] += gU[1]; cb[11] += gU[2]; cb[12] += dsig; cb[13] += drho;
+                                }
+                            }
+                            __syncthreads();
+                        }
+                        // one record per entry -> the slot's accumulator row (waves 0-1, lane = entry)
+                        if (wave < 2 && valid) {
+                            const float* cb = comb + e * 16;
+                            bool any = false;
+                            for (int x = 0; x < 14; ++x) any |= cb[x] != 0.f;
+                            if (any) {
+                                const int gi = queue[e];
+                                const GaussRec rec = k.recs[gi];
+                                const float q[3] = {px - rec.a.x, py - rec.a.y, pz - rec.a.z};
+                                float rec32[kRec];
+                                for (int x = 0; x < kRec; ++x) rec32[x] = 0.f;
+                                // dA += (sum gU0) q^T; dmu = -A^T sum gU0 (+ the view-direction chain)
+                                for (int x = 0; x < 3; ++x)
+                                    for (int c = 0; c < 3; ++c) rec32[3 * x + c] = fmaf(cb[9 + x], q[c], cb[3 * x + c]);
+                                for (int c = 0; c < 3; ++c)
+                                    rec32[9 + c] = -(A[c] * cb[9] + A[3 + c] * cb[10] + A[6 + c] * cb[11]);
+                                rec32[12] = cb[12];
+                                // rho = max(0, 0.5 + f.Y(dir)): the clamp passes where 0.5 + sh >= 0
+                                float dx, dy, dz, nrm;
+                                view_dir<NLOSGR_PRESET_CUDA>(-q[0], -q[1], -q[2], dx, dy, dz, nrm);
+                                float Y[kMaxK];
+                                sh_basis<NLOSGR_PRESET_CUDA>(deg, dx, dy, dz, Y);
+                                const float* f = k.g.features + (size_t)gi * k.g.k_feat;
+                                const float sh = sh_dot(f, Y, K);
+                                const float gr = sh + 0.5f >= 0.f ? cb[13] : 0.f;
+                                if (gr != 0.f) {
+#pragma unroll
+                                    for (int c = 0; c < kMaxK; ++c) rec32[16 + c] = c < K ? gr * Y[c] : 0.f;
+                                    float gx, gy, gz;
+                                    sh_grad_dir<NLOSGR_PRESET_CUDA>(deg, dx, dy, dz, f, gx, gy, gz);
+                                    float ox, oy, oz;
+                                    view_dir_bwd<NLOSGR_PRESET_CUDA>(-q[0], -q[1], -q[2], nrm, gr * gx, gr * gy, gr * gz,
+                                                                     ox, oy, oz);
+                                    rec32[9] += ox; rec32[10] += oy; rec32[11] += oz;
+                                }
+                                float4* dst = reinterpret_cast<float4*>(k.acc + ((size_t)blockIdx.x * k.g.ng + gi) * kRec);
+                                for (int x = 0; x < kRec / 4; ++x) {
+                                    float4 v = dst[x];
+                                    v.x += rec32[4 * x]; v.y += rec32[4 * x + 1]; v.z += rec32[4 * x + 2]; v.w += rec32[4 * x + 3];
+                                    dst[x] = v;
+                                }
+                            }
+                        }
+                        if (SEL == NLOSGR_SELECT_AABB) {
+                            // cap counters after the window: every staged hit of the ray
+                            __syncthreads();
+                            if (half == 1)
+                                for (int r = rg; r < RT; r += 4) {
+                                    const int i = ti0 + r / k.tj, j = tj0 + r % k.tj;
+                                    bool h = false;
+                                    if (valid && i < nt && j < np_) {
+                                        const float dx = sth[i] * cph[j], dy = sth[i] * sph[j], dz = cth[i];
+                                        h = slab_hit(sel6, px, py, pz, 1.0f / (dx + 1e-8f), 1.0f / (dy + 1e-8f),
+                                                     1.0f / (dz + 1e-8f));
+                                    }
+                                    const unsigned long long m = __builtin_amdgcn_ballot_w64(h);
+                                    if (lane == 0) icnt[r] = min(kCap, icnt[r] + ihalf[r] + __popcll(m));
+                                }
+                        }
+                    }
+                    __syncthreads();
+                    // drop the staged window from the queue
+                    const int rest = qn - nst;
+                    int keep = 0;
+                    if (tid < rest) keep = queue[nst + tid];
+                    __syncthreads();
+                    if (tid < rest) queue[tid] = keep;
+                    qn = rest;
+                    __syncthreads();
+                }
+            }
+
+            if (!pairs) {
+                // ---------------- scan: wave = ray, lane = bin ----------------
+                for (int r = wave; r < RT; r += kTW) {
+                    const int i = ti0 + r / k.tj, j = tj0 + r % k.tj;
+                    const bool rv = i < nt && j < np_;
+                    const float st = rv ? sth[i] : 0.f;
+                    const size_t ray = (size_t)p * nt * np_ + (size_t)(rv ? i : 0) * np_ + (rv ? j : 0);
+                    float2* row = rows + r * nr;
+                    float carry = 0.f;
+                    for (int c = 0; c < nch; ++c) {
+                        const int kb = c * 64 + lane;
+                        const bool in = kb < nr;
+                        const float2 dw = in ? row[kb] : make_float2(0.f, 0.f);
+                        float out, T = 1.f;
+                        if (OCCL) {
+                            const float x = dw.x * cdt;
+                            const float incl = wave_incl_sum(x);
+                            T = fast_exp2(-(carry + incl - x) * kLog2e);
+                            out = T >= 1e-4f ? T * dw.y : 0.f;
+                            if (!(T >= 1e-4f)) T = 0.f;
+                            carry += __shfl(incl, 63);
+                        } else {
+                            out = dw.y;
+                        }
+                        if (!BWD) {
+                            if (k.ray_out && rv && in) k.ray_out[ray * nr + kb] = out * k.opt.ray_scale;
+                            if (in) row[kb].x = rv ? out * st : 0.f;
+                        } else {
+                            float gk = 0.f;
+                            if (rv && in) {
+                                if (k.grad_hist) gk = k.grad_hist[(size_t)p * nr + kb] * k.geo.att[kb] * k.geo.hscale[p] * st;
+                                if (k.grad_ray) gk += k.grad_ray[ray * nr + kb] * k.opt.ray_scale;
+                            }
+                            // a = dL/dW; E = dL/dout out (suffix-summed into dL/dD below)
+                            if (in) row[kb] = OCCL ? make_float2(gk * T, gk * out) : make_float2(gk, 0.f);
+                        }
+                    }
+                    if (BWD && OCCL) {
+                        float suffix = 0.f;
+                        for (int c = nch - 1; c >= 0; --c) {
+                            const int kb = c * 64 + lane;
+                            const bool in = kb < nr;
+                            const float E = in ? row[kb].y : 0.f;
+                            const float incl = wave_incl_suffix(E);
+                            if (in) row[kb].y = -cdt * (suffix + incl - E);
+                            suffix += __shfl(incl, 0);
+                        }
+                    }
+                }
+                __syncthreads();
+                if (!BWD) {
+                    float* hp = k.hpart + ((size_t)p * k.ntiles + t) * nr;
+                    for (int kb = tid; kb < nr; kb += kTB) {
+                        float s = 0.f;
+                        for (int r = 0; r < RT; ++r) s += rows[r * nr + kb].x;
+                        hp[kb] = s;
+                    }
+                }
+            }
+        }
+    }
+}
+
+// hist[p][k] = (sum over tiles in order) x att[k] x hscale[p]
+__global__ __launch_bounds__(256) void tiles_reduce_kernel(const float* __restrict__ hpart, int ntiles, long long P, int nr,
+                                                           const float* __restrict__ att, const float* __restrict__ hscale,
+                                                           float* __restrict__ hist) {
+    const long long x = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= P * nr) return;
+    const long long p = x / nr;
+    const int kb = (int)(x - p * nr);
+    float s = 0.f;
+    for (int t = 0; t < ntiles; ++t) s += hpart[(p * ntiles + t) * nr + kb];
+    hist[x] = s * att[kb] * hscale[p];
+}
+
+// per Gaussian: sum of the slot rows in slot order, chained to the raw parameters
+__global__ __launch_bounds__(256) void tiles_finish_kernel(TArgs k, float* d_mu, float* d_scaling, float* d_rot,
+                                                           float* d_opac, float* d_feat) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= k.g.ng) return;
+    float a[kRec];
+    for (int x = 0; x < kRec; ++x) a[x] = 0.f;
+    for (int s = 0; s < k.nslot; ++s) {
+        const float4* src = reinterpret_cast<const float4*>(k.acc + ((size_t)s * k.g.ng + i) * kRec);
+        for (int x = 0; x < kRec / 4; ++x) {
+            const float4 v = src[x];
+            a[4 * x] += v.x; a[4 * x + 1] += v.y; a[4 * x + 2] += v.z; a[4 * x + 3] += v.w;
+        }
+    }
+    d_mu[3 * i] = a[9]; d_mu[3 * i + 1] = a[10]; d_mu[3 * i + 2] = a[11];
+    const float sg = 1.0f / (1.0f + expf(-k.g.opacity[i]));
+    d_opac[i] = a[12] * sg * (1.0f - sg);
+    const int K = (k.g.sh_degree + 1) * (k.g.sh_degree + 1);
+    for (int c = 0; c < k.g.k_feat; ++c) d_feat[(size_t)i * k.g.k_feat + c] = c < K ? a[16 + c] : 0.f;
+    chain_to_raw<NLOSGR_PRESET_CUDA>(k.g, i, a, d_scaling, d_rot);
+}
+
+int cu_count() {
+    static int n = 0;
+    if (n == 0) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            n <= 0)
+            n = 256;
+    }
+    return n;
+}
+
+struct TPlan {
+    int rt, ti, tj, nti, ntj, ntiles, nslot;
+    long long nitems;
+    size_t off_cull, off_bbox, off_acc, off_hpart, total;
+};
+
+TPlan plan(const nlosgr_gaussians* g, const nlosgr_geometry* geo) {
+    TPlan P;
+    P.rt = tile_rays(geo->nr);
+    int ti = 1;
+    while (ti * ti < P.rt) ti <<= 1;          // TI >= TJ, TI * TJ = RT
+    P.ti = ti;
+    P.tj = P.rt / ti;
+    P.nti = (geo->nt + P.ti - 1) / P.ti;
+    P.ntj = (geo->np + P.tj - 1) / P.tj;
+    P.ntiles = P.nti * P.ntj;
+    P.nitems = (long long)geo->nwall * P.ntiles;
+    P.nslot = (int)(P.nitems < cu_count() ? P.nitems : cu_count());
+    if (P.nslot < 1) P.nslot = 1;
+    const size_t ng = g->ng > 0 ? (size_t)g->ng : 1;
+    P.off_cull = align_up(ng * sizeof(GaussRec));
+    P.off_bbox = P.off_cull + align_up(ng * sizeof(float4));
+    P.off_acc = P.off_bbox + align_up(ng * 6 * sizeof(float));
+    P.off_hpart = P.off_acc + align_up((size_t)P.nslot * ng * kRec * sizeof(float));
+    P.total = P.off_hpart + align_up((size_t)geo->nwall * P.ntiles * geo->nr * sizeof(float));
+    return P;
+}
+
+template <int SEL, bool DENSE, bool OCCL, bool BWD>
+void launch_tile(const TArgs& a, size_t shm, hipStream_t s) {
+    hipLaunchKernelGGL((tile_kernel<SEL, DENSE, OCCL, BWD>), dim3(a.nslot), dim3(kTB), shm, s, a);
+}
+
+template <bool BWD>
+void dispatch_tile(const TArgs& a, size_t shm, hipStream_t s) {
+    const bool occl = a.opt.mode == NLOSGR_MODE_OCCL;
+    if (a.opt.selection == NLOSGR_SELECT_AABB) {
+        if (occl) launch_tile<NLOSGR_SELECT_AABB, false, true, BWD>(a, shm, s);
+        else launch_tile<NLOSGR_SELECT_AABB, false, false, BWD>(a, shm, s);
+    } else if (!(a.opt.cutoff > 0.f)) {
+        if (occl) launch_tile<NLOSGR_SELECT_SUPPORT, true, true, BWD>(a, shm, s);
+        else launch_tile<NLOSGR_SELECT_SUPPORT, true, false, BWD>(a, shm, s);
+    } else {
+        if (occl) launch_tile<NLOSGR_SELECT_SUPPORT, false, true, BWD>(a, shm, s);
+        else launch_tile<NLOSGR_SELECT_SUPPORT, false, false, BWD>(a, shm, s);
+    }
+}
+
+int prepare(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_options* opt, void* ws,
+            const TPlan& P, TArgs& a, hipStream_t s) {
+    memset(&a, 0, sizeof(a));
+    a.g = *g; a.geo = *geo; a.opt = *opt;
+    char* base = (char*)ws;
+    a.recs = (const GaussRec*)base;
+    a.cull = (const float4*)(base + P.off_cull);
+    a.bbox = (const float*)(base + P.off_bbox);
+    a.acc = (float*)(base + P.off_acc);
+    a.hpart = (float*)(base + P.off_hpart);
+    a.ti = P.ti; a.tj = P.tj; a.rt = P.rt;
+    a.ntile_i = P.nti; a.ntile_j = P.ntj; a.ntiles = P.ntiles;
+    a.nitems = P.nitems; a.nslot = P.nslot;
+    launch_preprocess(g, (GaussRec*)base, s);
+    HIPCHK(hipGetLastError());
+    const int nb = (g->ng + 255) / 256;
+    if (opt->selection == NLOSGR_SELECT_AABB)
+        hipLaunchKernelGGL(cull_prep_kernel<NLOSGR_SELECT_AABB>, dim3(nb), dim3(256), 0, s, *g, a.recs, opt->cutoff,
+                           (float4*)a.cull, (float*)a.bbox);
+    else
+        hipLaunchKernelGGL(cull_prep_kernel<NLOSGR_SELECT_SUPPORT>, dim3(nb), dim3(256), 0, s, *g, a.recs, opt->cutoff,
+                           (float4*)a.cull, (float*)a.bbox);
+    HIPCHK(hipGetLastError());
+    return NLOSGR_OK;
+}
+
+}  // namespace
+
+namespace nlosgr {
+namespace detail {
+
+bool tiles_engine(const nlosgr_options* opt) {
+    return opt->mode == NLOSGR_MODE_OCCL || opt->selection == NLOSGR_SELECT_AABB;
+}
+
+int tiles_validate(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_options* opt) {
+    if (g->preset != NLOSGR_PRESET_CUDA)
+        return set_err(NLOSGR_E_UNSUPPORTED, "occlusion compositing / AABB selection are path C semantics: cuda preset only");
+    if (opt->mode != NLOSGR_MODE_OCCL && opt->mode != NLOSGR_MODE_NOOCL)
+        return set_err(NLOSGR_E_UNSUPPORTED, "AABB selection supports the noocl and occl modes");
+    if (opt->selection != NLOSGR_SELECT_SUPPORT && opt->selection != NLOSGR_SELECT_AABB)
+        return set_err(NLOSGR_E_INVALID, "unknown selection");
+    if (geo->nr > 4096) return set_err(NLOSGR_E_UNSUPPORTED, "occl / AABB engine: nr <= 4096");
+    if ((size_t)TLayout(tile_rays(geo->nr), geo->nr).total * 4 > 160 * 1024)
+        return set_err(NLOSGR_E_UNSUPPORTED, "occl / AABB engine: LDS budget");
+    return NLOSGR_OK;
+}
+
+size_t tiles_workspace_bytes(const nlosgr_gaussians* g, const nlosgr_geometry* geo) { return plan(g, geo).total; }
+
+int tiles_fwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_options* opt, void* ws,
+              float* hist_out, float* ray_out, hipStream_t s) {
+    if (!ws) return set_err(NLOSGR_E_INVALID, "workspace is null");
+    const TPlan P = plan(g, geo);
+    if (ray_out) HIPCHK(hipMemsetAsync(ray_out, 0, (size_t)geo->nwall * geo->nt * geo->np * geo->nr * sizeof(float), s));
+    if (g->ng == 0) {
+        if (hist_out) HIPCHK(hipMemsetAsync(hist_out, 0, (size_t)geo->nwall * geo->nr * sizeof(float), s));
+        return NLOSGR_OK;
+    }
+    TArgs a;
+    int rc = prepare(g, geo, opt, ws, P, a, s);
+    if (rc) return rc;
+    a.hist_out = hist_out;
+    a.ray_out = ray_out;
+    const size_t shm = (size_t)TLayout(P.rt, geo->nr).total * sizeof(float);
+    dispatch_tile<false>(a, shm, s);
+    HIPCHK(hipGetLastError());
+    if (hist_out) {
+        const long long n = (long long)geo->nwall * geo->nr;
+        hipLaunchKernelGGL(tiles_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a.hpart, P.ntiles,
+                           (long long)geo->nwall, geo->nr, geo->att, geo->hscale, hist_out);
+        HIPCHK(hipGetLastError());
+    }
+    return NLOSGR_OK;
+}
+
+int tiles_bwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_options* opt, void* ws,
+              const float* grad_hist, const float* grad_ray, float* d_mu, float* d_scaling, float* d_rotation,
+              float* d_opacity, float* d_features, hipStream_t s) {
+    if (!ws) return set_err(NLOSGR_E_INVALID, "workspace is null");
+    const TPlan P = plan(g, geo);
+    TArgs a;
+    int rc = prepare(g, geo, opt, ws, P, a, s);
+    if (rc) return rc;
+    a.grad_hist = grad_hist;
+    a.grad_ray = grad_ray;
+    HIPCHK(hipMemsetAsync(a.acc, 0, (size_t)P.nslot * g->ng * kRec * sizeof(float), s));
+    if (geo->nwall > 0 && (grad_hist || grad_ray)) {
+        const size_t shm = (size_t)TLayout(P.rt, geo->nr).total * sizeof(float);
+        dispatch_tile<true>(a, shm, s);
+        HIPCHK(hipGetLastError());
+    }
+    hipLaunchKernelGGL(tiles_finish_kernel, dim3((g->ng + 255) / 256), dim3(256), 0, s, a, d_mu, d_scaling, d_rotation,
+                       d_opacity, d_features);
+    HIPCHK(hipGetLastError());
+    return NLOSGR_OK;
+}
+
+}  // namespace detail
+}  // namespace nlosgr

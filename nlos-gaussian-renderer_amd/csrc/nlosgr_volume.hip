@@ -1435,32 +1435,8 @@ template <int PRESET>
 __global__ __launch_bounds__(kBlock) void bbox_kernel(nlosgr_gaussians g, float sig, float* out) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= g.ng) return;
-    float s[3];
-    for (int t = 0; t < 3; ++t) s[t] = expf(g.scaling[3 * i + t]) * g.scaling_modifier;
-    const float* Q = g.rotation + 4 * i;
-    float n = sqrtf(Q[0] * Q[0] + Q[1] * Q[1] + Q[2] * Q[2] + Q[3] * Q[3]);
-    float R[9];
-    if (PRESET == NLOSGR_PRESET_CUDA && n < 1e-8f) {
-        R[0] = 1.f; R[1] = 0.f; R[2] = 0.f; R[3] = 0.f; R[4] = 1.f; R[5] = 0.f; R[6] = 0.f; R[7] = 0.f; R[8] = 1.f;
-    } else {
-        if (PRESET == NLOSGR_PRESET_TORCH) n = fmaxf(n, 1e-12f);
-        float q[4] = {Q[0] / n, Q[1] / n, Q[2] / n, Q[3] / n};
-        if (PRESET == NLOSGR_PRESET_TORCH) {
-            float n1 = sqrtf(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
-            for (int t = 0; t < 4; ++t) q[t] /= n1;
-        }
-        quat_rot(q[0], q[1], q[2], q[3], R);
-    }
-    for (int r = 0; r < 3; ++r) {
-        float v = 0.f;
-        for (int c = 0; c < 3; ++c) v += (R[3 * r + c] * s[c]) * (R[3 * r + c] * s[c]);
-        if (PRESET == NLOSGR_PRESET_TORCH) v = fmaxf(v, 1e-8f);
-        const float e = sig * sqrtf(v);
-        out[6 * i + r] = g.mu[3 * i + r] - e;
-        out[6 * i + 3 + r] = g.mu[3 * i + r] + e;
-    }
+    gauss_bbox<PRESET>(g, i, sig, out + 6 * (size_t)i);
 }
-
 
 // ------------------------------------------------------------------------------------------
 // host side
@@ -1477,7 +1453,8 @@ int validate(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr
         return set_err(NLOSGR_E_UNSUPPORTED, "active_sh_degree must be in [0, 3]");
     if (g->k_feat < (g->sh_degree + 1) * (g->sh_degree + 1) || g->k_feat > kMaxK)
         return set_err(NLOSGR_E_INVALID, "k_feat must satisfy (sh_degree+1)^2 <= k_feat <= 16");
-    if (opt->mode != NLOSGR_MODE_NOOCL && opt->mode != NLOSGR_MODE_NETF && opt->mode != NLOSGR_MODE_BININT)
+    if (opt->mode != NLOSGR_MODE_NOOCL && opt->mode != NLOSGR_MODE_NETF && opt->mode != NLOSGR_MODE_BININT &&
+        opt->mode != NLOSGR_MODE_OCCL)
         return set_err(NLOSGR_E_INVALID, "unknown mode");
     if (geo->nwall < 0 || geo->nt < 1 || geo->np < 1 || geo->nr < 1)
         return set_err(NLOSGR_E_INVALID, "bad geometry sizes");
@@ -1488,6 +1465,7 @@ int validate(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr
     if (geo->nwall > 0 && (!geo->wall || !geo->sin_theta || !geo->cos_theta || !geo->sin_phi ||
                            !geo->cos_phi || !geo->grid_lin || !geo->hscale || !geo->r || !geo->att))
         return set_err(NLOSGR_E_INVALID, "null geometry pointer");
+    if (tiles_engine(opt)) return tiles_validate(g, geo, opt);
     const size_t lds_f = (size_t)FwdLayout(geo->nr, geo->nt, geo->np).total * 4;
     const size_t lds_b = (size_t)BwdLayout(geo->nr, geo->nt, geo->np, bwd_shared(geo)).total * 4;
     if (lds_f > 160 * 1024 || lds_b > 160 * 1024) return set_err(NLOSGR_E_UNSUPPORTED, "problem exceeds LDS budget");
@@ -1695,6 +1673,7 @@ const char* nlosgr_last_error(void) { return g_err; }
 
 size_t nlosgr_workspace_bytes(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_options* opt) {
     if (validate(g, geo, opt) != NLOSGR_OK) return 0;
+    if (tiles_engine(opt)) return tiles_workspace_bytes(g, geo);
     const size_t rec = align_up((size_t)g->ng * sizeof(GaussRec));
     const size_t part = align_up((size_t)bwd_nsplit_ws(g, geo, opt) * g->ng * 32 * sizeof(float));
     return rec + part + cache_bytes(g, geo, opt) + sh_bytes(g, geo) + 256 + fpart_bytes(g, geo);
@@ -1705,6 +1684,7 @@ int nlosgr_render_fwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo, con
     const int rc = validate(g, geo, opt);
     if (rc) return rc;
     if (geo->nwall == 0 || (!hist_out && !ray_out)) return NLOSGR_OK;
+    if (tiles_engine(opt)) return tiles_fwd(g, geo, opt, workspace, hist_out, ray_out, (hipStream_t)hip_stream);
     return run_fwd(g, geo, opt, workspace, hist_out, ray_out, nullptr, (hipStream_t)hip_stream);
 }
 
@@ -1713,6 +1693,7 @@ int nlosgr_count_support(const nlosgr_gaussians* g, const nlosgr_geometry* geo, 
     const int rc = validate(g, geo, opt);
     if (rc) return rc;
     if (!counts) return set_err(NLOSGR_E_INVALID, "counts is null");
+    if (tiles_engine(opt)) return set_err(NLOSGR_E_UNSUPPORTED, "count_support: pair-major modes only");
     hipStream_t s = (hipStream_t)hip_stream;
     HIPCHK(hipMemsetAsync(counts, 0, 3 * sizeof(unsigned long long), s));
     if (geo->nwall == 0) return NLOSGR_OK;
@@ -1731,6 +1712,9 @@ int nlosgr_render_bwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo, con
     if (!workspace) return set_err(NLOSGR_E_INVALID, "workspace is null");
     if (!d_mu || !d_scaling || !d_rotation || !d_opacity || !d_features)
         return set_err(NLOSGR_E_INVALID, "null gradient output pointer");
+    if (tiles_engine(opt))
+        return tiles_bwd(g, geo, opt, workspace, grad_hist, grad_ray, d_mu, d_scaling, d_rotation, d_opacity,
+                         d_features, (hipStream_t)hip_stream);
     hipStream_t s = (hipStream_t)hip_stream;
     KArgs ka;
     memset(&ka, 0, sizeof(ka));

@@ -17,8 +17,12 @@ PRESET_CUDA = 1
 MODE_NOOCL = 0
 MODE_NETF = 1
 MODE_BININT = 2
+MODE_OCCL = 3
+SELECT_SUPPORT = 0
+SELECT_AABB = 1
 PRESETS = {"torch": PRESET_TORCH, "cuda": PRESET_CUDA}
-MODES = {"noocl": MODE_NOOCL, "netf": MODE_NETF, "binint": MODE_BININT}
+MODES = {"noocl": MODE_NOOCL, "netf": MODE_NETF, "binint": MODE_BININT, "occl": MODE_OCCL}
+SELECTIONS = {"support": SELECT_SUPPORT, "aabb": SELECT_AABB}
 
 _P = ctypes.c_void_p
 
@@ -39,7 +43,7 @@ class Geometry(ctypes.Structure):
 class Options(ctypes.Structure):
     _fields_ = [("mode", ctypes.c_int32), ("cutoff", ctypes.c_float), ("c_deltaT", ctypes.c_float),
                 ("ray_scale", ctypes.c_float), ("nsplit", ctypes.c_int32), ("flags", ctypes.c_int32),
-                ("ray_cache", ctypes.c_int32)]
+                ("ray_cache", ctypes.c_int32), ("selection", ctypes.c_int32)]
 
 
 class Rays(ctypes.Structure):
@@ -54,7 +58,7 @@ class AdamGroup(ctypes.Structure):
 
 ADAM_MAX_GROUPS = 8  # NLOSGR_ADAM_MAX_GROUPS
 MAX_PER_RAY = 256   # NLOSGR_MAX_PER_RAY
-ABI_VERSION = 4     # NLOSGR_ABI_VERSION
+ABI_VERSION = 5     # NLOSGR_ABI_VERSION
 
 # every symbol include/nlosgr.h declares (tests check the exports against this list)
 EXPORTS = ["nlosgr_workspace_bytes", "nlosgr_render_fwd", "nlosgr_render_bwd", "nlosgr_count_support",

@@ -22,7 +22,8 @@ RAY_CACHE_MAX_BYTES = int(float(os.environ.get("NLOSGR_RAY_CACHE_GB", "128")) * 
 @dataclass(frozen=True)
 class RenderConfig:
     preset: str = "torch"        # "torch" (path T) or "cuda" (path C)
-    mode: str = "noocl"          # "noocl", "netf" or "binint" (bin-integrated no-occlusion, forward only)
+    mode: str = "noocl"          # "noocl", "netf", "binint" (bin-integrated no-occlusion, forward only) or
+                                 # "occl" (path C shared-transmittance compositing, cuda preset)
     sh_degree: int = 0
     scaling_modifier: float = 1.0
     cutoff: float = 0.0          # Mahalanobis support radius; <= 0 -> dense
@@ -31,12 +32,14 @@ class RenderConfig:
     nsplit: int = 0
     flags: int = 0               # ablation / diagnostics only (0 in production)
     ray_cache: bool = True       # forward records in-support rays per pair for the backward
+    selection: str = "support"   # "support" (Mahalanobis cutoff) or "aabb" (path C's 3-sigma box filter,
+                                 # first 256 Gaussians per ray by index; cuda preset)
 
 
 def use_ray_cache(cfg, geo, ng, want_rays=False):
     """The forward->backward ray cache applies to culled, histogram-only, differentiable modes."""
     return (bool(cfg.ray_cache) and cfg.cutoff > 0 and not want_rays and cfg.mode in ("noocl", "netf")
-            and geo.nwall * ng * 24 <= RAY_CACHE_MAX_BYTES)
+            and cfg.selection == "support" and geo.nwall * ng * 24 <= RAY_CACHE_MAX_BYTES)
 
 
 def _as_f32(t):
@@ -62,7 +65,7 @@ def _structs(mu, scaling, rotation, opacity, features, geo, cfg, ray_cache=False
                        _lib.ptr(geo.cos_theta), _lib.ptr(geo.sin_phi), _lib.ptr(geo.cos_phi),
                        _lib.ptr(geo.grid_lin), _lib.ptr(geo.hscale), _lib.ptr(geo.r), _lib.ptr(geo.att))
     o = _lib.Options(_lib.MODES[cfg.mode], float(cfg.cutoff), float(cfg.c_deltaT), float(cfg.ray_scale),
-                     int(cfg.nsplit), int(cfg.flags), int(bool(ray_cache)))
+                     int(cfg.nsplit), int(cfg.flags), int(bool(ray_cache)), _lib.SELECTIONS[cfg.selection])
     return g, gs, o
 
 

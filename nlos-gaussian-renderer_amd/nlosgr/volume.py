@@ -66,10 +66,11 @@ def volume_loss(hist, target, reduction="mean"):
     return (d * d).mean() if reduction == "mean" else (d * d).sum()
 
 
-def make_config(model, scene, preset="cuda", mode="noocl", cutoff=0.0, scaling_modifier=1.0):
+def make_config(model, scene, preset="cuda", mode="noocl", cutoff=0.0, scaling_modifier=1.0, selection="support"):
     return RenderConfig(preset=preset, mode=mode, sh_degree=int(model.active_sh_degree),
                         scaling_modifier=scaling_modifier, cutoff=cutoff, c_deltaT=scene.c * scene.deltaT,
-                        ray_scale=(scene.c * scene.deltaT if (preset == "cuda" and mode in ("noocl", "binint")) else 1.0))
+                        ray_scale=(scene.c * scene.deltaT if (preset == "cuda" and mode in ("noocl", "binint")) else 1.0),
+                        selection=selection)
 
 
 def train_step(model, geo, cfg, target, loss_scale=1.0):
