@@ -45,6 +45,7 @@ CONFIGS = {
     "C5": (500_000, 256, 256, 2048, 32, False),
     "S1": (20_000, 32, 32, 512, 32, False),      # quick iteration size (not a BASELINE config)
 }
+PROGRESS = os.environ.get("NLOSGR_BENCH_PROGRESS") == "1"   # per-step lines on stderr (long profiled runs)
 PEAK_HBM_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
@@ -172,10 +173,13 @@ def timed_run(step, steps, warmup, world, dev):
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     phases = []
-    for _ in range(steps):
+    for i in range(steps):
         ev_fwd, ev_bwd = step()
         torch.cuda.synchronize(dev)
         phases.append((ev_fwd[0].elapsed_time(ev_fwd[1]), ev_bwd[0].elapsed_time(ev_bwd[1]) if ev_bwd else 0.0))
+        if PROGRESS:
+            print(f"[bench] step {i + 1}/{steps} fwd {phases[-1][0]:.1f} ms bwd {phases[-1][1]:.1f} ms",
+                  file=sys.stderr, flush=True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)

@@ -121,6 +121,9 @@ typedef struct {
     int32_t selection;        /* NLOSGR_SELECT_*.  OCCL mode and AABB selection run the ray-tile engine
                                  (ray-major, per-ray compositing, deterministic); the ray cache and
                                  nlosgr_count_support do not apply there */
+    int32_t g_begin, g_end;   /* backward only: gradients of Gaussians [g_begin, g_end) (g_begin % 256 == 0;
+                                 rows outside are left untouched), so a caller can all-reduce one
+                                 bucket while the next one is differentiated; g_end = 0 -> all */
 } nlosgr_options;
 
 /* Scratch bytes needed by fwd/bwd for this problem (caller allocates, 256-B aligned); includes

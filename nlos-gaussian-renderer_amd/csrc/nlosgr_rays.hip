@@ -13,9 +13,12 @@
 //            early exit (volume_renderer.cu:121-135).
 //   backward: wave = one ray (one wave per workgroup: per-sample adjoints live in LDS); suffix
 //            scan for dL/dD, then per Gaussian the sums over samples of dL/dpdf * pdf * z and
-//            * t z, reduced across the wave and added (global float atomics, 14 per ray and
-//            Gaussian) into per-Gaussian accumulators; a finish kernel chains them to the raw
-//            parameters (dA -> scaling/rotation, dsigma -> opacity, drho -> SH / view direction).
+//            * t z, reduced across the wave.  Deterministic: a persistent grid of nslot
+//            single-wave workgroups takes rays slot, slot + nslot, ... (static order) and adds
+//            each (ray, Gaussian) result into the slot's private accumulator row (plain
+//            read-modify-write, no atomics); a finish kernel sums the slot rows of each Gaussian
+//            in slot order and chains them to the raw parameters (dA -> scaling/rotation,
+//            dsigma -> opacity, drho -> SH / view direction).
 #include "nlosgr_common.hpp"
 
 using namespace nlosgr;
@@ -34,8 +37,18 @@ struct RArgs {
     const GaussRec* recs;
     const int32_t* filter;
     float cdt;
-    float* acc;   // backward accumulators [ng][16]: dA[9], dMu[3], dsigma, drho
+    float* acc;   // backward accumulators [nslot][ng][16]: dA[9], dMu[3], dsigma, drho
+    int nslot;
 };
+
+// backward slots: at most 1024 single-wave workgroups and 1 GiB of accumulator rows
+int rays_nslot(const nlosgr_gaussians* g, const nlosgr_rays* r) {
+    const long long per = (long long)(g->ng > 0 ? g->ng : 1) * 16 * sizeof(float);
+    long long n = (1ll << 30) / per;
+    if (n > 1024) n = 1024;
+    if (n > r->nrays) n = r->nrays;
+    return n < 1 ? 1 : (int)n;
+}
 
 // ------------------------------------------------------------------------------------------
 // AABB filter (first kMaxPerRay Gaussians by index whose box the half-infinite ray hits)
@@ -196,115 +209,117 @@ __global__ __launch_bounds__(64) void rays_bwd_kernel(RArgs k, const float* __re
     float* GW = GD + k.r.nsamp;                   // [ns] dL/dW_s (W = the albedo-weighted sum)
     float* LV = GW + k.r.nsamp;                   // [ns] 1 where the sample is live (occlusion)
     const int lane = lane_id();
-    const int ray = blockIdx.x;
-    const int32_t* row = k.filter + (size_t)ray * kRowLen;
-    const int n = min(max(row[0], 0), kMaxPerRay);
-    if (n == 0) return;
-    stage_ray<PRESET>(k, ray, row + 1, n, gd);
-    wave_sync();
-    const int ns = k.r.nsamp;
-    const float cdt = k.cdt;
-    const size_t rbase = (size_t)ray * ns;
-    if (!OCCL) {
-        for (int s = lane; s < ns; s += 64) {
-            GD[s] = g_dens ? g_dens[rbase + s] : 0.f;
-            GW[s] = g_rho ? g_rho[rbase + s] * cdt : 0.f;
-        }
-    } else {
-        // forward quantities, then dL/dD_s = g_D[s] - c dT sum_{s'>s} (g_rho rho + g_T T)_{s'}
-        // over live samples (T_s >= 1e-4; the others are constant 0), dL/dW_s = g_rho[s] T_s
-        float carry = 0.f;
-        for (int c0 = 0; c0 < ns; c0 += 64) {
-            const int s = c0 + lane;
-            const float t = s < ns ? k.r.t[s] : 0.f;
-            float D, W;
-            sample_sums<true>(gd, n, t, cdt, D, W);
-            if (s >= ns) D = W = 0.f;
-            const float x = D * cdt;
-            float incl = x;
-#pragma unroll
-            for (int off = 1; off < 64; off <<= 1) {
-                const float u = __shfl_up(incl, off);
-                if (lane >= off) incl += u;
+    float* acc_slot = k.acc + (size_t)blockIdx.x * k.g.ng * 16;
+    for (int ray = blockIdx.x; ray < k.r.nrays; ray += k.nslot) {
+        const int32_t* row = k.filter + (size_t)ray * kRowLen;
+        const int n = min(max(row[0], 0), kMaxPerRay);
+        if (n == 0) continue;
+        wave_sync();   // the previous ray is done with the LDS tables
+        stage_ray<PRESET>(k, ray, row + 1, n, gd);
+        wave_sync();
+        const int ns = k.r.nsamp;
+        const float cdt = k.cdt;
+        const size_t rbase = (size_t)ray * ns;
+        if (!OCCL) {
+            for (int s = lane; s < ns; s += 64) {
+                GD[s] = g_dens ? g_dens[rbase + s] : 0.f;
+                GW[s] = g_rho ? g_rho[rbase + s] * cdt : 0.f;
             }
-            const float T = expf(-(carry + incl - x));
-            const bool live = s < ns && T >= 1e-4f;
-            const float gr = live && g_rho ? g_rho[rbase + s] : 0.f;
-            const float gt = live && g_tr ? g_tr[rbase + s] : 0.f;
-            if (s < ns) {
-                GW[s] = gr * T;
-                GD[s] = gr * T * W + gt * T;           // E_s, suffix-scanned below
-                LV[s] = live ? 1.f : 0.f;
+        } else {
+            // forward quantities, then dL/dD_s = g_D[s] - c dT sum_{s'>s} (g_rho rho + g_T T)_{s'}
+            // over live samples (T_s >= 1e-4; the others are constant 0), dL/dW_s = g_rho[s] T_s
+            float carry = 0.f;
+            for (int c0 = 0; c0 < ns; c0 += 64) {
+                const int s = c0 + lane;
+                const float t = s < ns ? k.r.t[s] : 0.f;
+                float D, W;
+                sample_sums<true>(gd, n, t, cdt, D, W);
+                if (s >= ns) D = W = 0.f;
+                const float x = D * cdt;
+                float incl = x;
+    #pragma unroll
+                for (int off = 1; off < 64; off <<= 1) {
+                    const float u = __shfl_up(incl, off);
+                    if (lane >= off) incl += u;
+                }
+                const float T = expf(-(carry + incl - x));
+                const bool live = s < ns && T >= 1e-4f;
+                const float gr = live && g_rho ? g_rho[rbase + s] : 0.f;
+                const float gt = live && g_tr ? g_tr[rbase + s] : 0.f;
+                if (s < ns) {
+                    GW[s] = gr * T;
+                    GD[s] = gr * T * W + gt * T;           // E_s, suffix-scanned below
+                    LV[s] = live ? 1.f : 0.f;
+                }
+                carry += __shfl(incl, 63);
             }
-            carry += __shfl(incl, 63);
+            wave_sync();
+            float suffix = 0.f;   // sum of E over later chunks
+            for (int ch = (ns + 63) / 64 - 1; ch >= 0; --ch) {
+                const int s = ch * 64 + lane;
+                const float E = s < ns ? GD[s] : 0.f;
+                float incl = E;   // inclusive suffix sum within the chunk
+    #pragma unroll
+                for (int off = 1; off < 64; off <<= 1) {
+                    const float u = __shfl_down(incl, off);
+                    if (lane + off < 64) incl += u;
+                }
+                if (s < ns) {
+                    const float gdn = g_dens ? g_dens[rbase + s] : 0.f;
+                    GD[s] = LV[s] != 0.f ? gdn - cdt * (suffix + incl - E) : 0.f;
+                }
+                suffix += __shfl(incl, 0);
+            }
         }
         wave_sync();
-        float suffix = 0.f;   // sum of E over later chunks
-        for (int ch = (ns + 63) / 64 - 1; ch >= 0; --ch) {
-            const int s = ch * 64 + lane;
-            const float E = s < ns ? GD[s] : 0.f;
-            float incl = E;   // inclusive suffix sum within the chunk
-#pragma unroll
-            for (int off = 1; off < 64; off <<= 1) {
-                const float u = __shfl_down(incl, off);
-                if (lane + off < 64) incl += u;
+        const float ox = k.r.origins[3 * ray], oy = k.r.origins[3 * ray + 1], oz = k.r.origins[3 * ray + 2];
+        const float dxr = k.r.dirs[3 * ray], dyr = k.r.dirs[3 * ray + 1], dzr = k.r.dirs[3 * ray + 2];
+        for (int e = 0; e < n; ++e) {
+            const float4 a = *reinterpret_cast<const float4*>(gd + e * kGD);
+            const float4 b = *reinterpret_cast<const float4*>(gd + e * kGD + 4);
+            const float sig = b.z, rho = b.w;
+            float Sz0 = 0.f, Sz1 = 0.f, Sz2 = 0.f, St0 = 0.f, St1 = 0.f, St2 = 0.f, dsig = 0.f, drho = 0.f;
+            for (int s = lane; s < ns; s += 64) {
+                const float t = k.r.t[s];
+                const float z0 = fmaf(t, a.w, a.x), z1 = fmaf(t, b.x, a.y), z2 = fmaf(t, b.y, a.z);
+                const float m2 = fmaf(z0, z0, fmaf(z1, z1, z2 * z2));
+                const float pdf = fast_exp2(-kHalfLog2e * m2);
+                const float contrib = sig * pdf;
+                const float gD = GD[s], gW = GW[s];
+                float dW_dc, wterm;   // dW/dcontrib and W's per-Gaussian term / rho
+                if (OCCL) {
+                    const float em = expf(-contrib * cdt);
+                    dW_dc = rho * cdt * em;
+                    wterm = -expm1f(-contrib * cdt);
+                } else {
+                    dW_dc = rho;
+                    wterm = contrib;
+                }
+                const float gc = gD + gW * dW_dc;       // dL/dcontrib
+                const float G = gc * sig * pdf;          // dL/dpdf * pdf
+                Sz0 = fmaf(G, z0, Sz0); Sz1 = fmaf(G, z1, Sz1); Sz2 = fmaf(G, z2, Sz2);
+                St0 = fmaf(G * t, z0, St0); St1 = fmaf(G * t, z1, St1); St2 = fmaf(G * t, z2, St2);
+                dsig = fmaf(gc, pdf, dsig);
+                drho = fmaf(gW, wterm, drho);
             }
-            if (s < ns) {
-                const float gdn = g_dens ? g_dens[rbase + s] : 0.f;
-                GD[s] = LV[s] != 0.f ? gdn - cdt * (suffix + incl - E) : 0.f;
+            Sz0 = wave_sum(Sz0); Sz1 = wave_sum(Sz1); Sz2 = wave_sum(Sz2);
+            St0 = wave_sum(St0); St1 = wave_sum(St1); St2 = wave_sum(St2);
+            dsig = wave_sum(dsig); drho = wave_sum(drho);
+            if (lane == 0) {
+                // pdf = exp(-|z|^2/2), z = u0 + t v:  dL/du0 = -sum G z,  dL/dv = -sum G t z
+                const int gi = row[1 + e];
+                const GaussRec rec = k.recs[gi];
+                const float A[9] = {rec.b.x, rec.b.y, rec.b.z, rec.b.w, rec.c.x, rec.c.y, rec.c.z, rec.c.w, rec.d.x};
+                const float q[3] = {ox - rec.a.x, oy - rec.a.y, oz - rec.a.z};
+                const float d3[3] = {dxr, dyr, dzr};
+                const float dU[3] = {-Sz0, -Sz1, -Sz2}, dV[3] = {-St0, -St1, -St2};
+                float* acc = acc_slot + (size_t)gi * 16;
+                for (int r = 0; r < 3; ++r)
+                    for (int c = 0; c < 3; ++c) acc[3 * r + c] += dV[r] * d3[c] + dU[r] * q[c];
+                for (int c = 0; c < 3; ++c) acc[9 + c] += -(A[c] * dU[0] + A[3 + c] * dU[1] + A[6 + c] * dU[2]);
+                acc[12] += dsig;
+                acc[13] += drho;
             }
-            suffix += __shfl(incl, 0);
-        }
-    }
-    wave_sync();
-    const float ox = k.r.origins[3 * ray], oy = k.r.origins[3 * ray + 1], oz = k.r.origins[3 * ray + 2];
-    const float dxr = k.r.dirs[3 * ray], dyr = k.r.dirs[3 * ray + 1], dzr = k.r.dirs[3 * ray + 2];
-    for (int e = 0; e < n; ++e) {
-        const float4 a = *reinterpret_cast<const float4*>(gd + e * kGD);
-        const float4 b = *reinterpret_cast<const float4*>(gd + e * kGD + 4);
-        const float sig = b.z, rho = b.w;
-        float Sz0 = 0.f, Sz1 = 0.f, Sz2 = 0.f, St0 = 0.f, St1 = 0.f, St2 = 0.f, dsig = 0.f, drho = 0.f;
-        for (int s = lane; s < ns; s += 64) {
-            const float t = k.r.t[s];
-            const float z0 = fmaf(t, a.w, a.x), z1 = fmaf(t, b.x, a.y), z2 = fmaf(t, b.y, a.z);
-            const float m2 = fmaf(z0, z0, fmaf(z1, z1, z2 * z2));
-            const float pdf = fast_exp2(-kHalfLog2e * m2);
-            const float contrib = sig * pdf;
-            const float gD = GD[s], gW = GW[s];
-            float dW_dc, wterm;   // dW/dcontrib and W's per-Gaussian term / rho
-            if (OCCL) {
-                const float em = expf(-contrib * cdt);
-                dW_dc = rho * cdt * em;
-                wterm = -expm1f(-contrib * cdt);
-            } else {
-                dW_dc = rho;
-                wterm = contrib;
-            }
-            const float gc = gD + gW * dW_dc;       // dL/dcontrib
-            const float G = gc * sig * pdf;          // dL/dpdf * pdf
-            Sz0 = fmaf(G, z0, Sz0); Sz1 = fmaf(G, z1, Sz1); Sz2 = fmaf(G, z2, Sz2);
-            St0 = fmaf(G * t, z0, St0); St1 = fmaf(G * t, z1, St1); St2 = fmaf(G * t, z2, St2);
-            dsig = fmaf(gc, pdf, dsig);
-            drho = fmaf(gW, wterm, drho);
-        }
-        Sz0 = wave_sum(Sz0); Sz1 = wave_sum(Sz1); Sz2 = wave_sum(Sz2);
-        St0 = wave_sum(St0); St1 = wave_sum(St1); St2 = wave_sum(St2);
-        dsig = wave_sum(dsig); drho = wave_sum(drho);
-        if (lane == 0) {
-            // pdf = exp(-|z|^2/2), z = u0 + t v:  dL/du0 = -sum G z,  dL/dv = -sum G t z
-            const int gi = row[1 + e];
-            const GaussRec rec = k.recs[gi];
-            const float A[9] = {rec.b.x, rec.b.y, rec.b.z, rec.b.w, rec.c.x, rec.c.y, rec.c.z, rec.c.w, rec.d.x};
-            const float q[3] = {ox - rec.a.x, oy - rec.a.y, oz - rec.a.z};
-            const float d3[3] = {dxr, dyr, dzr};
-            const float dU[3] = {-Sz0, -Sz1, -Sz2}, dV[3] = {-St0, -St1, -St2};
-            float* acc = k.acc + (size_t)gi * 16;
-            for (int r = 0; r < 3; ++r)
-                for (int c = 0; c < 3; ++c) atomicAdd(acc + 3 * r + c, dV[r] * d3[c] + dU[r] * q[c]);
-            for (int c = 0; c < 3; ++c)
-                atomicAdd(acc + 9 + c, -(A[c] * dU[0] + A[3 + c] * dU[1] + A[6 + c] * dU[2]));
-            atomicAdd(acc + 12, dsig);
-            atomicAdd(acc + 13, drho);
         }
     }
 }
@@ -315,7 +330,9 @@ __global__ __launch_bounds__(kBlock) void rays_finish_kernel(RArgs k, float* d_m
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= k.g.ng) return;
     float acc[16];
-    for (int t = 0; t < 16; ++t) acc[t] = k.acc[(size_t)i * 16 + t];
+    for (int t = 0; t < 16; ++t) acc[t] = 0.f;
+    for (int s = 0; s < k.nslot; ++s)
+        for (int t = 0; t < 16; ++t) acc[t] += k.acc[((size_t)s * k.g.ng + i) * 16 + t];
     const float mx = k.g.mu[3 * i], my = k.g.mu[3 * i + 1], mz = k.g.mu[3 * i + 2];
     float dmu[3] = {acc[9], acc[10], acc[11]};
     const float drho = acc[13];
@@ -367,7 +384,8 @@ extern "C" {
 
 size_t nlosgr_rays_workspace_bytes(const nlosgr_gaussians* g, const nlosgr_rays* r) {
     if (validate_rays(g, r) != NLOSGR_OK) return 0;
-    return align_up((size_t)g->ng * sizeof(GaussRec)) + align_up((size_t)g->ng * 16 * sizeof(float)) + 256;
+    return align_up((size_t)g->ng * sizeof(GaussRec)) +
+           align_up((size_t)rays_nslot(g, r) * g->ng * 16 * sizeof(float)) + 256;
 }
 
 int nlosgr_filter_rays(const nlosgr_gaussians* g, const nlosgr_rays* r, const float* bboxes, int32_t* filter_out,
@@ -425,10 +443,11 @@ int nlosgr_rays_bwd(const nlosgr_gaussians* g, const nlosgr_rays* r, const int32
     memset(&k, 0, sizeof(k));
     k.g = *g; k.r = *r; k.recs = (const GaussRec*)workspace; k.filter = filter; k.cdt = c_deltaT;
     k.acc = (float*)((char*)workspace + align_up((size_t)g->ng * sizeof(GaussRec)));
+    k.nslot = rays_nslot(g, r);
     launch_preprocess(g, (GaussRec*)workspace, s);
-    HIPCHK(hipMemsetAsync(k.acc, 0, (size_t)g->ng * 16 * sizeof(float), s));
+    HIPCHK(hipMemsetAsync(k.acc, 0, (size_t)k.nslot * g->ng * 16 * sizeof(float), s));
     if (r->nrays > 0 && r->nsamp > 0 && (g_rho || g_density || g_trans)) {
-        const dim3 grid(r->nrays);
+        const dim3 grid(k.nslot);
         if (g->preset == NLOSGR_PRESET_TORCH) {
             if (use_occlusion) hipLaunchKernelGGL((rays_bwd_kernel<0, true>), grid, dim3(64), shm, s, k, g_rho, g_density, g_trans);
             else hipLaunchKernelGGL((rays_bwd_kernel<0, false>), grid, dim3(64), shm, s, k, g_rho, g_density, g_trans);

@@ -43,7 +43,8 @@ class Geometry(ctypes.Structure):
 class Options(ctypes.Structure):
     _fields_ = [("mode", ctypes.c_int32), ("cutoff", ctypes.c_float), ("c_deltaT", ctypes.c_float),
                 ("ray_scale", ctypes.c_float), ("nsplit", ctypes.c_int32), ("flags", ctypes.c_int32),
-                ("ray_cache", ctypes.c_int32), ("selection", ctypes.c_int32)]
+                ("ray_cache", ctypes.c_int32), ("selection", ctypes.c_int32), ("g_begin", ctypes.c_int32),
+                ("g_end", ctypes.c_int32)]
 
 
 class Rays(ctypes.Structure):

@@ -51,7 +51,7 @@ def _as_f32(t):
     return t.contiguous()
 
 
-def _structs(mu, scaling, rotation, opacity, features, geo, cfg, ray_cache=False):
+def _structs(mu, scaling, rotation, opacity, features, geo, cfg, ray_cache=False, g_range=None):
     ng = mu.shape[0]
     k_feat = features.shape[1] if features.dim() == 2 else 0
     if mu.shape != (ng, 3) or scaling.shape != (ng, 3) or rotation.shape != (ng, 4):
@@ -65,7 +65,8 @@ def _structs(mu, scaling, rotation, opacity, features, geo, cfg, ray_cache=False
                        _lib.ptr(geo.cos_theta), _lib.ptr(geo.sin_phi), _lib.ptr(geo.cos_phi),
                        _lib.ptr(geo.grid_lin), _lib.ptr(geo.hscale), _lib.ptr(geo.r), _lib.ptr(geo.att))
     o = _lib.Options(_lib.MODES[cfg.mode], float(cfg.cutoff), float(cfg.c_deltaT), float(cfg.ray_scale),
-                     int(cfg.nsplit), int(cfg.flags), int(bool(ray_cache)), _lib.SELECTIONS[cfg.selection])
+                     int(cfg.nsplit), int(cfg.flags), int(bool(ray_cache)), _lib.SELECTIONS[cfg.selection],
+                     *(g_range if g_range is not None else (0, 0)))
     return g, gs, o
 
 
@@ -96,23 +97,25 @@ def render_forward(mu, scaling, rotation, opacity, features, geo, cfg, want_hist
 
 
 def render_backward(mu, scaling, rotation, opacity, features, geo, cfg, grad_hist=None, grad_rays=None,
-                    workspace=None, ray_cache=False):
+                    workspace=None, ray_cache=False, g_range=None, out=None):
     """Gradients of the five raw parameter tensors.  ray_cache: `workspace` holds the ray record of
-    a forward of the same inputs (render_forward(..., ray_cache=True))."""
+    a forward of the same inputs (render_forward(..., ray_cache=True)).  g_range=(g0, g1) restricts
+    the backward to Gaussians [g0, g1) (g0 % 256 == 0) and writes only those rows of `out`, a
+    preallocated (d_mu, d_scaling, d_rotation, d_opacity, d_features) tuple (allocated if None)."""
     lib = _lib.load()
     dev = mu.device
     mu, scaling, rotation, opacity, features = [_as_f32(t) for t in (mu, scaling, rotation, opacity, features)]
-    g, gs, o = _structs(mu, scaling, rotation, opacity, features, geo, cfg, ray_cache)
+    g, gs, o = _structs(mu, scaling, rotation, opacity, features, geo, cfg, ray_cache, g_range)
     if ray_cache and workspace is None:
         raise ValueError("nlosgr: ray_cache backward needs the forward's workspace")
     ws = _workspace(lib, g, gs, o, dev) if workspace is None else workspace
     gh = grad_hist.float().contiguous() if grad_hist is not None else None
     gr = grad_rays.float().contiguous() if grad_rays is not None else None
-    d_mu = torch.empty_like(mu)
-    d_s = torch.empty_like(scaling)
-    d_q = torch.empty_like(rotation)
-    d_o = torch.empty(mu.shape[0], device=dev)
-    d_f = torch.empty_like(features)
+    if out is None:
+        d_mu, d_s, d_q = torch.empty_like(mu), torch.empty_like(scaling), torch.empty_like(rotation)
+        d_o, d_f = torch.empty(mu.shape[0], device=dev), torch.empty_like(features)
+    else:
+        d_mu, d_s, d_q, d_o, d_f = out
     _lib.check(lib.nlosgr_render_bwd(g, gs, o, _lib.ptr(ws), _lib.ptr(gh), _lib.ptr(gr), _lib.ptr(d_mu),
                                      _lib.ptr(d_s), _lib.ptr(d_q), _lib.ptr(d_o), _lib.ptr(d_f),
                                      _lib.stream_handle(dev)))

@@ -105,6 +105,46 @@ def allreduce_step(grads, loss4, n_total, group=None, async_op=False):
     return finish()
 
 
+def bucket_bounds(ng, nbuckets):
+    """Gaussian ranges [g0, g1) of the bucketed gradient exchange; g0 is a multiple of 256 (the
+    backward's Gaussian-block granularity, nlosgr_options.g_begin)."""
+    if nbuckets <= 1 or ng <= 256:
+        return [(0, ng)]
+    step = ((ng + nbuckets - 1) // nbuckets + 255) // 256 * 256
+    return [(g0, min(ng, g0 + step)) for g0 in range(0, ng, step)]
+
+
+class BucketedAllReduce:
+    """SURVEY §8e overlap: the six gradient tensors (GROUPS order, rows = Gaussians) are exchanged in
+    Gaussian buckets.  launch(b) packs rows [g0, g1) of every tensor into one contiguous buffer on the
+    current stream and issues an asynchronous all-reduce(SUM) of it (RCCL orders it after the work
+    already queued, so it runs while the next bucket is differentiated); finish() waits for all
+    buckets and writes the sums back into the tensors."""
+
+    def __init__(self, grads, bounds, group=None):
+        self.grads, self.bounds, self.group = grads, bounds, group
+        self.works, self.bufs = [], []
+
+    def launch(self, b):
+        g0, g1 = self.bounds[b]
+        buf = torch.cat([g[g0:g1].reshape(-1) for g in self.grads])
+        self.bufs.append((b, buf))
+        self.works.append(dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True))
+
+    def finish(self):
+        for w in self.works:
+            w.wait()
+        for b, buf in self.bufs:
+            g0, g1 = self.bounds[b]
+            off = 0
+            for g in self.grads:
+                n = (g1 - g0) * (g[0].numel() if g.dim() > 1 else 1)
+                g[g0:g1].copy_(buf[off:off + n].view_as(g[g0:g1]))
+                off += n
+        self.works, self.bufs = [], []
+        return self.grads
+
+
 class Adam:
     """torch.optim.Adam (no weight decay / amsgrad) on the device for a fixed list of contiguous
     fp32 tensors, one launch per step (nlosgr_adam)."""
@@ -147,7 +187,7 @@ class TrainStep:
     """
 
     def __init__(self, model, geo, cfg, target, gt_times=1.0, opt=None, spatial_lr_scale=1.0, nwall_total=None,
-                 group=None, sh_schedule=False, events=None):
+                 group=None, sh_schedule=False, events=None, buckets=4):
         self.model, self.geo, self.cfg = model, geo, cfg
         self.target = target.detach().float().contiguous()
         self.gt_times = float(gt_times)
@@ -164,6 +204,7 @@ class TrainStep:
         self.n_total = (nwall_total if nwall_total is not None else geo.nwall) * geo.nr
         self.sh_schedule = sh_schedule
         self.events = events      # optional {"fwd": (start, end), "bwd": (start, end)} HIP events (bench timing)
+        self.buckets = int(buckets)   # gradient all-reduce buckets overlapped with the backward (world > 1)
         self.iteration = 0
         ng = model._mu.shape[0]
         self._tensors = [model._mu.data, model._features_dc.data.view(ng, -1), model._features_rest.data.view(ng, -1),
@@ -213,13 +254,34 @@ class TrainStep:
         loss2 = loss4[:2]
         if ev:
             ev["bwd"][0].record(stream)
-        d_mu, d_s, d_q, d_o, d_f = render_backward(*args, cfg, grad_hist=grad, workspace=ws, ray_cache=cache)
-        if ev:
-            ev["bwd"][1].record(stream)
-        del ws
-        grads = [d_mu, d_f[:, :1], d_f[:, 1:], d_o, d_s, d_q]
-        if self.world > 1:
-            grads, loss2 = allreduce_step(grads, loss4, self.n_total, self.group)
+        bounds = bucket_bounds(ng, self.buckets) if (self.world > 1 and cfg.mode != "occl"
+                                                     and cfg.selection == "support") else [(0, ng)]
+        if len(bounds) > 1:
+            # bucketed: differentiate Gaussians [g0, g1), then all-reduce that bucket asynchronously
+            # while the next bucket's backward runs (SURVEY §8e overlap)
+            outs = (torch.empty_like(args[0]), torch.empty_like(args[1]), torch.empty_like(args[2]),
+                    torch.empty(ng, device=m._mu.device), torch.empty_like(feats))
+            d_mu, d_s, d_q, d_o, d_f = outs
+            ex = BucketedAllReduce([d_mu, d_f[:, :1], d_f[:, 1:], d_o, d_s, d_q], bounds, self.group)
+            for b, gr in enumerate(bounds):
+                render_backward(*args, cfg, grad_hist=grad, workspace=ws, ray_cache=cache, g_range=gr, out=outs)
+                ex.launch(b)
+            sums = loss4[2:4].clone()
+            dist.all_reduce(sums, op=dist.ReduceOp.SUM, group=self.group)
+            if ev:
+                ev["bwd"][1].record(stream)
+            grads = ex.finish()
+            se, st = sums[0], sums[1]
+            loss2 = torch.stack([se / float(self.n_total), torch.where(st > 0, se / st, torch.zeros_like(se))])
+            del ws
+        else:
+            d_mu, d_s, d_q, d_o, d_f = render_backward(*args, cfg, grad_hist=grad, workspace=ws, ray_cache=cache)
+            if ev:
+                ev["bwd"][1].record(stream)
+            del ws
+            grads = [d_mu, d_f[:, :1], d_f[:, 1:], d_o, d_s, d_q]
+            if self.world > 1:
+                grads, loss2 = allreduce_step(grads, loss4, self.n_total, self.group)
         if self.opt.regularization:
             # + opacity_reg mean|sigmoid(o)| + scale_reg mean|exp(s)| (main.py:204-208); replicated
             # terms, so added after the all-reduce.  equal_loss stays the render term's (as there).

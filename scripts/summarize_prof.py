@@ -6,7 +6,8 @@
                            wave64 instruction / (128 SIMDs per XCD x GRBM_GUI_ACTIVE), GRBM_GUI_ACTIVE
                            being the sum over the 8 XCDs of each XCD's busy cycles (so 1024 SIMDs x
                            GRBM/8).  Transcendentals issue for longer, so this is a lower bound.
-  <tag>_sq_counters.csv    the raw SQ/GRBM rows of this library's kernels
+  <tag>_sq_counters.csv    the raw SQ/GRBM rows of this library's kernels (LDS pass counters merged
+                           into <tag>_valu.json per kernel)
   <tag>_bench.json         the bench line of the same command
 
     python scripts/summarize_prof.py gpurun_out/prof_c3 r02_c3
@@ -65,6 +66,10 @@ def main(src, tag):
     sqf = glob.glob(os.path.join(src, "sq_*counter_collection.csv"))
     if sqf:
         sq = per_kernel(sqf[0])
+        for f in glob.glob(os.path.join(src, "lds_*counter_collection.csv")):   # LDS pass, merged per kernel
+            for kname, c in per_kernel(f).items():
+                for n, v in c.items():
+                    sq[kname].setdefault(n, v)
         kern = {}
         for k, c in sq.items():
             if not ours(k):

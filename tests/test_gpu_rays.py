@@ -192,3 +192,24 @@ def test_nlos_gaussian_renderer_dropin(occl):
     bb = bboxes(m._mu, m._scaling, m._rotation, 1.0, 3.0, preset="cuda")
     got = rend.filter_gaussians(o.to(dev), d.to(dev), m._mu, bb).cpu()
     assert torch.equal(got, R.aabb_filter(o, d, bb.reshape(-1, 6).cpu()))
+
+
+@pytest.mark.parametrize("occl", [False, True])
+def test_rays_backward_deterministic(occl):
+    """The rays backward has no atomics: slot-private rows (static ray schedule) summed in slot order,
+    so two runs are bitwise identical (round 1 used global float atomics)."""
+    from nlosgr.rays import gaussian_filter, rays_backward
+    dev = torch.device("cuda:0")
+    m, o, d = _scene(300, 700, 5, scale_shift=1.5, opac_shift=1.0, deg=2)
+    t = torch.linspace(0.1, 1.4, 96, device=dev)
+    cam = torch.tensor([0.0, 0.0, 0.0], device=dev)
+    feats = torch.cat([m._features_dc, m._features_rest], dim=1)[:, :, 0].detach().contiguous()
+    filt = gaussian_filter(o, d, m._mu, m._scaling, m._rotation)
+    g = torch.Generator().manual_seed(1)
+    g_rho = torch.randn(o.shape[0], t.shape[0], generator=g).to(dev)
+    args = (o, d, t, m._mu, m._scaling, m._rotation, m._opacity, feats, cam, 2, 0.05, 1.0, occl, filt, g_rho, None, None)
+    r1 = rays_backward(*args)
+    r2 = rays_backward(*args)
+    for a, b in zip(r1, r2):
+        assert torch.isfinite(a).all()
+        assert torch.equal(a, b)

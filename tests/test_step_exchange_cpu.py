@@ -121,3 +121,42 @@ def test_allreduce_step_world2_matches_single_process():
         torch.testing.assert_close(loss2[0], loss, rtol=1e-6, atol=0)
         torch.testing.assert_close(loss2[1], eq, rtol=1e-6, atol=0)
         assert torch.isfinite(loss2).all()
+
+
+def _bucket_worker(rank, world, port, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from nlosgr.train import BucketedAllReduce, bucket_bounds
+        ng, K = 1000, 16
+        g = torch.Generator().manual_seed(10 + rank)
+        grads = [torch.randn(ng, 3, generator=g), torch.randn(ng, 1, generator=g), torch.randn(ng, K - 1, generator=g),
+                 torch.randn(ng, generator=g), torch.randn(ng, 3, generator=g), torch.randn(ng, 4, generator=g)]
+        mine = [t.clone() for t in grads]
+        bounds = bucket_bounds(ng, 3)
+        ex = BucketedAllReduce(grads, bounds, None)
+        for b in range(len(bounds)):
+            ex.launch(b)          # TrainStep interleaves these with the per-bucket backward
+        out[rank] = ([t.clone() for t in ex.finish()], mine, bounds)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bucketed_allreduce_world2():
+    """BucketedAllReduce (TrainStep's overlapped exchange) sums every row of all six
+    gradient tensors across ranks, bucket by bucket, back into the same tensors."""
+    from nlosgr.train import bucket_bounds
+    assert bucket_bounds(1000, 3) == [(0, 512), (512, 1000)]
+    assert bucket_bounds(100_000, 4)[0] == (0, 25_088) and bucket_bounds(100_000, 4)[-1][1] == 100_000
+    assert all(b0 % 256 == 0 for b0, _ in bucket_bounds(123_457, 7))
+    world = 2
+    port = _free_port()
+    out = mp.Manager().dict()
+    mp.spawn(_bucket_worker, args=(world, port, out), nprocs=world, join=True)
+    summed = [a + b for a, b in zip(out[0][1], out[1][1])]
+    for r in range(world):
+        got, _, bounds = out[r]
+        assert len(bounds) == 2
+        for a, b in zip(got, summed):
+            torch.testing.assert_close(a, b)
