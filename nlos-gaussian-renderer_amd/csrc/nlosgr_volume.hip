@@ -547,13 +547,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
                 continue;
             }
             if (!anymore && qcount == 0 && have) break;   // next Gaussians; segments carry over
-            // claims.  Vector (float2) drain: one winner per bank slot of each 16-lane group — the lane
-            // groups of ds_write_b64 (MI355X_MICROARCH.md §LDS: 4 x 16 lanes, bank (a/4) mod 32) — so
-            // the winners' start pairs are distinct mod 16 within every group: conflict-free stores
-            // (at most 2-way ds_read_b64), and distinct addresses.  Scalar drains: distinct start bins.
+            // claim distinct start keys (distinct addresses; vector drain: distinct start pairs)
             constexpr bool QUAD = MODE == NLOSGR_MODE_NOOCL && !RAYS && !DENSE;
             constexpr int VW = 2;   // bins per LDS read-add-write of the vector drain (float2)
-            const int key = QUAD ? (((lane >> 4) << 4) | ((d.pos / VW) & 15)) : d.pos;
+            const int key = QUAD ? (d.pos / VW) : d.pos;
             if (act) owner[key] = (unsigned char)lane;
             wave_sync();
             const bool win = act && owner[key] == (unsigned char)lane;
@@ -1101,9 +1098,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
         int ci = i0, cj = j0, qhead = 0, qcount = 0;
         unsigned round = 0;
         bool act = false, pend = false;
-        // per-pair sums of the handed-over ray results (see the hand-off): P0 = sum S0,
-        // Pa = sum alpha d, Pb = sum beta d d^T (symmetric: 00 01 02 11 12 22)
-        float P0 = 0.f, Pa[3] = {0.f, 0.f, 0.f}, Pb[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, drho_pair = 0.f;
+        float dU0p[3] = {0.f, 0.f, 0.f}, drho_pair = 0.f, s0_pair = 0.f;
         BRay b;
         b.pos = 0; b.rem = 0; b.slot = lane; b.ij = 0; b.kl = 0; b.len = 0;
         b.kap = b.kap0 = b.c0 = b.c2 = b.st = 0.f;
@@ -1112,8 +1107,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
         b.rho = b.sigma = 0.f;
         b.T = b.T0 = b.Etot = b.pre = b.dsig = b.drho = 0.f;
         b.ph1 = false;
-        // pending result of a finished ray: S0, alpha, beta (+ dsigma, drho in netf)
-        float rS = 0.f, rA = 0.f, rB = 0.f, rSig = 0.f, rRho = 0.f;
+        // pending result of a finished ray: dL/du0, dL/dv, dsigma, drho
+        float rU[3] = {0.f, 0.f, 0.f}, rV[3] = {0.f, 0.f, 0.f}, rSig = 0.f, rRho = 0.f;
         while (true) {
             if (CACHE && qcount < 64 && __builtin_amdgcn_ballot_w64((cbits0 | cbits1) != 0ull)) {
                 wave_sync();
@@ -1255,22 +1250,24 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
                         }
                     }
                     if (b.rem <= 0 && !pend) {
-                        // pdf = exp(-|z|^2/2), z = z* + dl v, z* = u0 + t* v, v = A d:
-                        //   dL/du0 = -(S0 u0 + alpha v),  dL/dv = -(alpha u0 + beta v)
-                        // with alpha = t* S0 + S1, beta = t* alpha + t* S1 + S2; so the pair needs only
-                        // sum S0, sum alpha d and sum beta d d^T (three scalars handed over per ray)
+                        // pdf = exp(-|z|^2/2), z = z* + dl v:  dL/du0 = -sum P z,  dL/dv = -sum P dl z
                         float S0 = b.S0, S1 = b.S1 * dr, S2 = b.S2 * dr * dr;
                         if (MODE == NLOSGR_MODE_NOOCL) {
                             if (!RAYS) { S0 *= b.st; S1 *= b.st; S2 *= b.st; }
-                            // no-occlusion: every term carries the pair's w; dsigma = S0 rho and
-                            // drho = S0 sigma — the pair lane applies w, rho and sigma to its sums
+                            // no-occlusion: dsigma = S0 rho, drho = S0 sigma; the pair lane applies its own
+                            // rho and sigma to the summed S0 (one value handed over instead of two)
+                            rSig = S0;
+                            rRho = 0.f;
+                            S0 *= b.w; S1 *= b.w; S2 *= b.w;
                         } else {
                             rSig = b.dsig;
                             rRho = b.drho;
                         }
-                        rS = S0;
-                        rA = fmaf(b.ts, S0, S1);
-                        rB = fmaf(b.ts, rA + S1, S2);
+                        for (int r = 0; r < 3; ++r) {
+                            const float zv = S0 * b.zs[r] + S1 * b.v[r];
+                            rU[r] = -zv;
+                            rV[r] = -(b.ts * zv + S1 * b.zs[r] + S2 * b.v[r]);
+                        }
                         act = false;
                         pend = !(k.opt.flags & 32);   // flags 32 (diagnostics): drop results, no hand-off
                     }
@@ -1288,22 +1285,24 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
                 const int src = got ? (int)(ow & 63u) : lane;
                 const bool won = pend && owner[b.slot] == stamp;
                 const float gm = got ? 1.f : 0.f;
+                float gU[3], gV[3];
                 // every lane must execute the bpermute: it cannot read lanes that are inactive in EXEC
-                const float gS = gm * __shfl(rS, src);
-                const float gA = gm * __shfl(rA, src);
-                const float gB = gm * __shfl(rB, src);
+#pragma unroll
+                for (int c = 0; c < 3; ++c) { gU[c] = gm * __shfl(rU[c], src); gV[c] = gm * __shfl(rV[c], src); }
+                const float gSig = gm * __shfl(rSig, src);
+                const float gRho = MODE == NLOSGR_MODE_NOOCL ? 0.f : gm * __shfl(rRho, src);
                 const int sij = __shfl(b.ij, src);
                 const int gij = got ? sij : 0;
                 const float2 th = tth[gij & 0xFFFF], ph = tph[gij >> 16];
                 const float d3[3] = {th.x * ph.x, th.x * ph.y, th.y};
-                P0 += gS;
-                for (int c = 0; c < 3; ++c) Pa[c] = fmaf(gA, d3[c], Pa[c]);
-                const float bd0 = gB * d3[0], bd1 = gB * d3[1];
-                Pb[0] = fmaf(bd0, d3[0], Pb[0]); Pb[1] = fmaf(bd0, d3[1], Pb[1]); Pb[2] = fmaf(bd0, d3[2], Pb[2]);
-                Pb[3] = fmaf(bd1, d3[1], Pb[3]); Pb[4] = fmaf(bd1, d3[2], Pb[4]); Pb[5] = fmaf(gB * d3[2], d3[2], Pb[5]);
-                if (MODE != NLOSGR_MODE_NOOCL) {
-                    dSig += gm * __shfl(rSig, src);
-                    drho_pair += gm * __shfl(rRho, src);
+                for (int r = 0; r < 3; ++r)
+                    for (int c = 0; c < 3; ++c) dA[3 * r + c] += gV[r] * d3[c];
+                for (int r = 0; r < 3; ++r) dU0p[r] += gU[r];
+                if (MODE == NLOSGR_MODE_NOOCL) {
+                    s0_pair += gSig;
+                } else {
+                    dSig += gSig;
+                    drho_pair += gRho;
                 }
                 wave_sync();
                 if (won) pend = false;
@@ -1315,27 +1314,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
         // sh_kernel from the stored dL/drho, which keeps 16 feature accumulators out of this kernel
         if (MODE == NLOSGR_MODE_NOOCL && active) {
             const float4 wrs = reinterpret_cast<const float4*>(pdat + lane * 16)[3];   // w, rho, sigma
-            dSig += P0 * wrs.y;
-            drho_pair = P0 * wrs.z;
+            dSig += s0_pair * wrs.y;
+            drho_pair = s0_pair * wrs.z;
         }
         if (active && wpair > 0.f) {
             const float q[3] = {px - mu[0], py - mu[1], pz - mu[2]};
             const float4* d4 = reinterpret_cast<const float4*>(pdat + lane * 16);
             const float4 a = d4[0], c = d4[1], e = d4[2];
             const float A[9] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w, e.x};
-            const float u0[3] = {e.y, e.z, e.w};
-            const float ws = MODE == NLOSGR_MODE_NOOCL ? wpair : 1.f;
-            const float Bs[9] = {Pb[0], Pb[1], Pb[2], Pb[1], Pb[3], Pb[4], Pb[2], Pb[4], Pb[5]};
-            float gU[3];
             for (int r = 0; r < 3; ++r)
-                gU[r] = -ws * fmaf(P0, u0[r], A[3 * r] * Pa[0] + A[3 * r + 1] * Pa[1] + A[3 * r + 2] * Pa[2]);
-            // dA += sum_rays dL/dv d^T + dL/du0 q^T = -w (u0 Pa^T + A Pb) + gU q^T
-            for (int r = 0; r < 3; ++r)
-                for (int cc = 0; cc < 3; ++cc) {
-                    const float apb = A[3 * r] * Bs[cc] + A[3 * r + 1] * Bs[3 + cc] + A[3 * r + 2] * Bs[6 + cc];
-                    dA[3 * r + cc] += fmaf(gU[r], q[cc], -ws * fmaf(u0[r], Pa[cc], apb));
-                }
-            for (int cc = 0; cc < 3; ++cc) dMu[cc] -= A[cc] * gU[0] + A[3 + cc] * gU[1] + A[6 + cc] * gU[2];
+                for (int cc = 0; cc < 3; ++cc) dA[3 * r + cc] += dU0p[r] * q[cc];
+            for (int cc = 0; cc < 3; ++cc) dMu[cc] -= A[cc] * dU0p[0] + A[3 + cc] * dU0p[1] + A[6 + cc] * dU0p[2];
         }
         if (active) k.drho[(size_t)p * k.g.ng + gi] = (wpair > 0.f && !(k.opt.flags & 64)) ? drho_pair : 0.f;
     }
