@@ -17,6 +17,9 @@ from . import _lib
 
 # upper bound on the forward->backward ray cache (24 B per wall point x Gaussian pair; C3: 39 GB)
 RAY_CACHE_MAX_BYTES = int(float(os.environ.get("NLOSGR_RAY_CACHE_GB", "128")) * 2 ** 30)   # of 288 GB HBM
+# the cache pays at small supports and costs at large ones (C3 backward, MI355X: 3 sigma 280 ms with the
+# cache vs 308 without; 5.7 sigma 1608 vs 1392 — the cached walk and the hand-off both slowed down)
+RAY_CACHE_MAX_CUTOFF = float(os.environ.get("NLOSGR_RAY_CACHE_MAX_CUTOFF", "4.5"))
 
 
 @dataclass(frozen=True)
@@ -38,8 +41,9 @@ class RenderConfig:
 
 def use_ray_cache(cfg, geo, ng, want_rays=False):
     """The forward->backward ray cache applies to culled, histogram-only, differentiable modes."""
-    return (bool(cfg.ray_cache) and cfg.cutoff > 0 and not want_rays and cfg.mode in ("noocl", "netf")
-            and cfg.selection == "support" and geo.nwall * ng * 24 <= RAY_CACHE_MAX_BYTES)
+    return (bool(cfg.ray_cache) and 0 < cfg.cutoff <= RAY_CACHE_MAX_CUTOFF and not want_rays
+            and cfg.mode in ("noocl", "netf") and cfg.selection == "support"
+            and geo.nwall * ng * 24 <= RAY_CACHE_MAX_BYTES)
 
 
 def _as_f32(t):

@@ -149,25 +149,27 @@ def test_c2_full_size():
 
 def test_c3_full_size_train_step_parity():
     """C3 (the headline): 100k Gaussians -> 128x128 wall x 1024 bins, cuda preset, cutoff 5.7 sigma,
-    forward recording the ray cache + backward walking it (the bench's path).  Whole volume finite;
+    forward + backward exactly as TrainStep runs them (the ray cache per use_ray_cache).  Whole volume finite;
     2 wall points vs the dense HIP evaluation (hist and gradients seeded there); a Gaussian subset vs
     the oracle."""
     from nlosgr import GaussianParams
-    from nlosgr.render import render_backward, render_forward
+    from nlosgr.render import render_backward, render_forward, use_ray_cache
     from nlosgr.volume import Scene, make_config
     dev = torch.device("cuda:0")
     scene = Scene(H=128, W=128, T=1024, ns=32)
     m = GaussianParams.synthetic(100_000, 3, preset="cuda", device=dev, seed=0)
     geo = scene.geometry(dev, "cuda", "noocl")
     cfg = make_config(m, scene, "cuda", "noocl", cutoff=PARITY_CUTOFF)
-    hist, _, ws = render_forward(*_params(m), geo, cfg, ray_cache=True)
+    cache = use_ray_cache(cfg, geo, 100_000)          # as TrainStep decides it (off at 5.7 sigma)
+    out = render_forward(*_params(m), geo, cfg, ray_cache=cache)
+    hist, ws = out[0], (out[2] if cache else None)
     _finite_volume(hist)
     idx = torch.tensor([128 * 40 + 30, 128 * 100 + 90], device=dev)
     g = torch.Generator().manual_seed(3)
     gseed = torch.randn(len(idx), 1024, generator=g).to(dev)
     gfull = torch.zeros(128 * 128, 1024, device=dev)
     gfull[idx] = gseed
-    d = render_backward(*_params(m), geo, cfg, grad_hist=gfull, workspace=ws, ray_cache=True)
+    d = render_backward(*_params(m), geo, cfg, grad_hist=gfull, workspace=ws, ray_cache=cache)
     del ws
     for t in d:
         assert torch.isfinite(t).all()
