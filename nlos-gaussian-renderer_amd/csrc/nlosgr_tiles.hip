@@ -12,9 +12,10 @@
 // (dense when cutoff <= 0), as the pair-major kernels do.
 //
 // Work item = (wall point p, ray tile t): a TI x TJ block of the (theta, phi) ray grid, sized so
-// the tile's [ray][bin] float2 rows fill 128 KB of LDS.  Persistent grid, one 8-wave workgroup per
-// CU; slot s takes items s, s + nslot, ... (a static schedule, so every sum has a fixed order).
-//   cull  : the 8 waves test 512 Gaussians per round (lane = Gaussian) against the tile's cone with
+// the tile's [ray][bin] float2 rows fill 128 KB of LDS.  Persistent grid, one workgroup per CU
+// (forward 16 waves, backward 8); slot s takes items s, s + nslot, ... (a static schedule, so every
+// sum has a fixed order).
+//   cull  : the waves test one Gaussian per lane per round against the tile's cone with
 //           the bounding sphere of the support (or of the box); passing indices queue in LDS in
 //           index order.
 //   stage : 128 queued Gaussians at a time become pair records in LDS (A, u0 = A(p - mu), quadric
@@ -34,6 +35,8 @@
 //   finish: sums each Gaussian's slot rows in slot order and chains to the raw parameters.
 #include <hip/hip_runtime.h>
 #include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "nlosgr_common.hpp"
@@ -43,10 +46,15 @@ using namespace nlosgr::detail;
 
 namespace {
 
-constexpr int kTB = 512;               // threads per workgroup (8 waves)
-constexpr int kTW = kTB / 64;
+// threads per workgroup: forward 16 waves (one ray of a 16-ray tile each), backward 8 waves
+// (its pair pass keeps more state per lane)
+template <bool BWD>
+constexpr int tile_threads() { return BWD ? 512 : 1024; }
 constexpr int kWin = 128;              // staged Gaussians per window
-constexpr int kQCap = kTB + kWin;      // queue capacity (indices)
+#ifndef NLOSGR_TILES_DIAG_BUILD
+#define NLOSGR_TILES_DIAG_BUILD 0          // per-phase cycle counters (a diagnostic build, NLOSGR_TILES_DIAG=1)
+#endif
+constexpr bool kDiag = NLOSGR_TILES_DIAG_BUILD;
 constexpr int kStage = 20;             // floats per staged pair: A[9] u0[3] sel[6] sigma rho
 constexpr int kRec = 32;               // floats per accumulator row: dA[9] dmu[3] dsigma pad[3] dF[16]
 constexpr int kCap = NLOSGR_MAX_PER_RAY;
@@ -71,6 +79,7 @@ struct TArgs {
     int ntile_i, ntile_j, ntiles;
     long long nitems;
     int nslot;
+    unsigned long long* diag;   // NLOSGR_TILES_DIAG: per-phase cycles of thread 0, summed over workgroups
 };
 
 __host__ __device__ inline int tile_rays(int nr) {
@@ -81,11 +90,11 @@ __host__ __device__ inline int tile_rays(int nr) {
 
 struct TLayout {   // offsets in floats
     int rows, stage, queue, comb, misc, total;
-    __host__ __device__ TLayout(int rt, int nr) {
+    __host__ __device__ TLayout(int rt, int nr, int tb) {
         rows = 0;
         stage = rows + 2 * rt * nr;
         queue = stage + kWin * kStage;
-        comb = queue + kQCap;
+        comb = queue + tb + kWin;          // queue capacity: one cull round + one window
         misc = comb + kWin * 16;
         total = misc + 256;
     }
@@ -181,10 +190,12 @@ __global__ __launch_bounds__(256) void cull_prep_kernel(nlosgr_gaussians g, cons
 // the tile kernel (forward: BWD = false; backward: BWD = true)
 // ------------------------------------------------------------------------------------------
 template <int SEL, bool DENSE, bool OCCL, bool BWD>
-__global__ __launch_bounds__(kTB) void tile_kernel(TArgs k) {
+__global__ __launch_bounds__(tile_threads<BWD>()) void tile_kernel(TArgs k) {
+    constexpr int kTB = tile_threads<BWD>();
+    constexpr int kTW = kTB / 64;
     extern __shared__ __align__(16) float sm[];
     const int nr = k.geo.nr, nt = k.geo.nt, np_ = k.geo.np;
-    const TLayout L(k.rt, nr);
+    const TLayout L(k.rt, nr, kTB);
     float2* rows = reinterpret_cast<float2*>(sm + L.rows);
     float* stage = sm + L.stage;
     int* queue = reinterpret_cast<int*>(sm + L.queue);
@@ -192,7 +203,7 @@ __global__ __launch_bounds__(kTB) void tile_kernel(TArgs k) {
     float* misc = sm + L.misc;
     int* icnt = reinterpret_cast<int*>(misc);          // [64] AABB cap counters per ray
     int* ihalf = icnt + 64;                             // [64] per-window hits of the first staged half
-    int* iwave = icnt + 128;                            // [8] cull counts per wave
+    int* iwave = icnt + 128;                            // [16] cull counts per wave
     float* cone = misc + 144;                           // axis xyz, cos h, sin h, pass-all flag
     const int tid = threadIdx.x, wave = tid >> 6, lane = lane_id();
     const int RT = k.rt;
@@ -204,6 +215,14 @@ __global__ __launch_bounds__(kTB) void tile_kernel(TArgs k) {
     const int nch = (nr + 63) / 64;
     const int deg = k.g.sh_degree, K = (deg + 1) * (deg + 1);
 
+    unsigned long long tc = 0, tcull = 0, tstage = 0, trays = 0, tscan = 0, nwin = 0, nent = 0, nec = 0, nchk = 0;
+#define TDIAG(acc)                                   \
+    if (kDiag && k.diag && tid == 0) {               \
+        const unsigned long long t1 = clock64();     \
+        acc += t1 - tc;                              \
+        tc = t1;                                     \
+    }
+    if (kDiag && k.diag && tid == 0) tc = clock64();
     for (long long item = blockIdx.x; item < k.nitems; item += k.nslot) {
         const int p = (int)(item / k.ntiles);
         const int t = (int)(item - (long long)p * k.ntiles);
@@ -277,6 +296,7 @@ __global__ __launch_bounds__(kTB) void tile_kernel(TArgs k) {
                     for (int w = 0; w < kTW; ++w) tot += iwave[w];
                     qn += tot;
                     __syncthreads();
+                    TDIAG(tcull)
                 }
                 const bool last = g0 + kTB >= k.g.ng;
                 // ---- windows of up to 128 staged Gaussians ----
@@ -317,6 +337,8 @@ __global__ __launch_bounds__(kTB) void tile_kernel(TArgs k) {
                         o[19] = fmaxf(sh + 0.5f, 0.0f);
                     }
                     __syncthreads();
+                    TDIAG(tstage)
+                    ++nwin;
                     if (!pairs) {
                         // ---- rays: wave = ray, lane = staged entry, then lane = bin ----
                         for (int r = wave; r < RT; r += kTW) {
@@ -365,12 +387,17 @@ __global__ __launch_bounds__(kTB) void tile_kernel(TArgs k) {
                                     rho = o[19];
                                 }
                                 const bool live = kl <= kh;
+                                if (kDiag && k.diag) {
+                                    const unsigned long long lm = __builtin_amdgcn_ballot_w64(live);
+                                    if (tid == 0) nent += __popcll(lm);
+                                }
                                 const int lo = wave_min_i(live ? kl : nr);
                                 const int hi = wave_max_i(live ? kh : -1);
                                 if (lo > hi) continue;
                                 for (int c = lo >> 6; c <= (hi >> 6); ++c) {
                                     unsigned long long cm =
                                         __builtin_amdgcn_ballot_w64(live && kl <= c * 64 + 63 && kh >= c * 64);
+                                    if (kDiag && k.diag && tid == 0) { ++nchk; nec += __popcll(cm); }
                                     if (!cm) continue;
                                     const int kb = c * 64 + lane;
                                     const float kf = (float)kb;
@@ -579,10 +606,12 @@ __global__ __launch_bounds__(kTB) void tile_kernel(TArgs k) {
                     if (tid < rest) queue[tid] = keep;
                     qn = rest;
                     __syncthreads();
+                    TDIAG(trays)
                 }
             }
 
             if (!pairs) {
+                TDIAG(trays)
                 // ---------------- scan: wave = ray, lane = bin ----------------
                 for (int r = wave; r < RT; r += kTW) {
                     const int i = ti0 + r / k.tj, j = tj0 + r % k.tj;
@@ -640,9 +669,21 @@ __global__ __launch_bounds__(kTB) void tile_kernel(TArgs k) {
                         hp[kb] = s;
                     }
                 }
+                TDIAG(tscan)
             }
         }
     }
+    if (kDiag && k.diag && tid == 0) {
+        atomicAdd(k.diag, tcull);
+        atomicAdd(k.diag + 1, tstage);
+        atomicAdd(k.diag + 2, trays);
+        atomicAdd(k.diag + 3, tscan);
+        atomicAdd(k.diag + 4, nwin);
+        atomicAdd(k.diag + 5, nent);
+        atomicAdd(k.diag + 6, nec);
+        atomicAdd(k.diag + 7, nchk);
+    }
+#undef TDIAG
 }
 
 // hist[p][k] = (sum over tiles in order) x att[k] x hscale[p]
@@ -721,11 +762,34 @@ TPlan plan(const nlosgr_gaussians* g, const nlosgr_geometry* geo) {
 
 template <int SEL, bool DENSE, bool OCCL, bool BWD>
 void launch_tile(const TArgs& a, size_t shm, hipStream_t s) {
-    hipLaunchKernelGGL((tile_kernel<SEL, DENSE, OCCL, BWD>), dim3(a.nslot), dim3(kTB), shm, s, a);
+    hipLaunchKernelGGL((tile_kernel<SEL, DENSE, OCCL, BWD>), dim3(a.nslot), dim3(tile_threads<BWD>()), shm, s, a);
 }
 
 template <bool BWD>
-void dispatch_tile(const TArgs& a, size_t shm, hipStream_t s) {
+void dispatch_tile_(const TArgs& a, size_t shm, hipStream_t s);
+
+// NLOSGR_TILES_DIAG=1 (diagnostics only): per-phase cycles of each workgroup's thread 0, printed
+template <bool BWD>
+void dispatch_tile(const TArgs& a0, size_t shm, hipStream_t s) {
+    if (!kDiag || !getenv("NLOSGR_TILES_DIAG")) {
+        dispatch_tile_<BWD>(a0, shm, s);
+        return;
+    }
+    TArgs a = a0;
+    unsigned long long h[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    if (hipMalloc(&a.diag, sizeof(h)) != hipSuccess) return;
+    (void)hipMemcpyAsync(a.diag, h, sizeof(h), hipMemcpyHostToDevice, s);
+    dispatch_tile_<BWD>(a, shm, s);
+    (void)hipMemcpyAsync(h, a.diag, sizeof(h), hipMemcpyDeviceToHost, s);
+    (void)hipStreamSynchronize(s);
+    (void)hipFree(a.diag);
+    fprintf(stderr, "[tiles %s] slot-cycles cull %.3g stage %.3g windows %.3g scan %.3g windows %llu (slots %d); "
+            "wave 0: entries %llu entry-chunks %llu chunks %llu\n",
+            BWD ? "bwd" : "fwd", (double)h[0], (double)h[1], (double)h[2], (double)h[3], h[4], a.nslot, h[5], h[6], h[7]);
+}
+
+template <bool BWD>
+void dispatch_tile_(const TArgs& a, size_t shm, hipStream_t s) {
     const bool occl = a.opt.mode == NLOSGR_MODE_OCCL;
     if (a.opt.selection == NLOSGR_SELECT_AABB) {
         if (occl) launch_tile<NLOSGR_SELECT_AABB, false, true, BWD>(a, shm, s);
@@ -782,7 +846,7 @@ int tiles_validate(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const 
     if (opt->selection != NLOSGR_SELECT_SUPPORT && opt->selection != NLOSGR_SELECT_AABB)
         return set_err(NLOSGR_E_INVALID, "unknown selection");
     if (geo->nr > 4096) return set_err(NLOSGR_E_UNSUPPORTED, "occl / AABB engine: nr <= 4096");
-    if ((size_t)TLayout(tile_rays(geo->nr), geo->nr).total * 4 > 160 * 1024)
+    if ((size_t)TLayout(tile_rays(geo->nr), geo->nr, tile_threads<false>()).total * 4 > 160 * 1024)
         return set_err(NLOSGR_E_UNSUPPORTED, "occl / AABB engine: LDS budget");
     return NLOSGR_OK;
 }
@@ -803,7 +867,7 @@ int tiles_fwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosg
     if (rc) return rc;
     a.hist_out = hist_out;
     a.ray_out = ray_out;
-    const size_t shm = (size_t)TLayout(P.rt, geo->nr).total * sizeof(float);
+    const size_t shm = (size_t)TLayout(P.rt, geo->nr, tile_threads<false>()).total * sizeof(float);
     dispatch_tile<false>(a, shm, s);
     HIPCHK(hipGetLastError());
     if (hist_out) {
@@ -827,7 +891,7 @@ int tiles_bwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosg
     a.grad_ray = grad_ray;
     HIPCHK(hipMemsetAsync(a.acc, 0, (size_t)P.nslot * g->ng * kRec * sizeof(float), s));
     if (geo->nwall > 0 && (grad_hist || grad_ray)) {
-        const size_t shm = (size_t)TLayout(P.rt, geo->nr).total * sizeof(float);
+        const size_t shm = (size_t)TLayout(P.rt, geo->nr, tile_threads<true>()).total * sizeof(float);
         dispatch_tile<true>(a, shm, s);
         HIPCHK(hipGetLastError());
     }
