@@ -67,6 +67,26 @@ __device__ __forceinline__ void sh_basis(int deg, float x, float y, float z, flo
     }
 }
 
+// sum_c f[c] Y_c(x,y,z) for c < (deg+1)^2, accumulated in c order without a Y[] array: the degree
+// tests are uniform branches and f (registers or a global row) is read only below (deg+1)^2.
+template <int PRESET>
+__device__ __forceinline__ float sh_dot(int deg, float x, float y, float z, const float* f) {
+    float s = f[0] * kSH_C0;
+    if (deg < 1) return s;
+    const float sg = PRESET == NLOSGR_PRESET_TORCH ? -1.0f : 1.0f;
+    s += f[1] * (sg * kSH_C1 * y);
+    s += f[2] * (kSH_C1 * z);
+    s += f[3] * (sg * kSH_C1 * x);
+    if (deg < 2) return s;
+    float Y[16];
+    sh_basis<PRESET>(deg < 3 ? 2 : 3, x, y, z, Y);
+    s += f[4] * Y[4]; s += f[5] * Y[5]; s += f[6] * Y[6]; s += f[7] * Y[7]; s += f[8] * Y[8];
+    if (deg < 3) return s;
+#pragma unroll
+    for (int c = 9; c < 16; ++c) s += f[c] * Y[c];
+    return s;
+}
+
 // d/d(x,y,z) of sum_c f[c] Y_c(x,y,z) (same polynomial forms as sh_basis).
 template <int PRESET>
 __device__ __forceinline__ void sh_grad_dir(int deg, float x, float y, float z, const float* f,

@@ -129,14 +129,7 @@ __device__ __forceinline__ void pair_setup(const KArgs& k, const float* f, const
     P.q[0] = px - mu[0]; P.q[1] = py - mu[1]; P.q[2] = pz - mu[2];
     for (int r = 0; r < 3; ++r) P.u0[r] = P.A[3 * r] * P.q[0] + P.A[3 * r + 1] * P.q[1] + P.A[3 * r + 2] * P.q[2];
     view_dir<PRESET>(-P.q[0], -P.q[1], -P.q[2], P.dir[0], P.dir[1], P.dir[2], P.nrm);
-    const int deg = k.g.sh_degree;
-    const int K = (deg + 1) * (deg + 1);
-    float Y[kMaxK];
-    sh_basis<PRESET>(deg, P.dir[0], P.dir[1], P.dir[2], Y);
-    float sh = 0.f;
-#pragma unroll
-    for (int c = 0; c < kMaxK; ++c)
-        if (c < K) sh += f[c] * Y[c];
+    const float sh = sh_dot<PRESET>(k.g.sh_degree, P.dir[0], P.dir[1], P.dir[2], f);
     P.sh = sh;
     P.rho = fmaxf(sh + 0.5f, 0.0f);
     P.w = P.sigma * P.rho;
@@ -482,18 +475,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
         P.i0 = P.i1 = P.j0 = P.j1 = 0;
         if (have) {
             const int gi = base + lane;
-            // all of the chunk's record and feature loads issued together, ahead of the setup math
-            GaussRec nrec;
-            float nfeat[kMaxK];
-            {
-                const int gl = min(gi, k.g.ng - 1);
-                nrec = k.recs[gl];
-                load_feat(k.g, gl, nfeat);
-            }
+            // the record is loaded ahead of the setup math; the SH coefficients are read from global
+            // inside the albedo sum (a register copy of the row spilled the setup at 80 VGPRs)
+            const int gl = min(gi, k.g.ng - 1);
+            const GaussRec nrec = k.recs[gl];
             if (gi < g_hi) {
                 float mu[3];
                 load_rec(nrec, P, mu);
-                pair_setup<PRESET, DENSE>(k, nfeat, mu, px, py, pz, lin, mc2, P);
+                pair_setup<PRESET, DENSE>(k, k.g.features + (size_t)gl * k.g.k_feat, mu, px, py, pz, lin, mc2, P);
                 more = (P.w > 0.f) && P.i0 <= P.i1 && P.j0 <= P.j1;
                 lw = more ? flog2(P.w) : 0.f;
                 sc = P.sigma * cdt;
@@ -894,8 +883,16 @@ __device__ __forceinline__ void load_pdat(const float* pd, float* A, float* u0, 
 
 // grow[k] = dL/dhist[p,k] att[k] hscale[p], zero-padded to nr + kBSteps.  Rows of nr % 4 == 0
 // are staged with 16-B loads issued together (one memory round trip per 1024 bins per lane).
+// lane index the compiler cannot hoist: per-wall-point staging addresses are recomputed (a few
+// VALU ops) instead of being kept live across the backward's wall-point loop (they spilled)
+__device__ __forceinline__ int lane_opaque() {
+    int l = lane_id();
+    __asm__ __volatile__("" : "+v"(l));
+    return l;
+}
+
 __device__ __forceinline__ void stage_grow(const float* grad, const float* att, float hs, int nr, float* grow) {
-    const int lane = lane_id();
+    const int lane = lane_opaque();
     if (grad && (nr & 3) == 0 && ((reinterpret_cast<uintptr_t>(grad) | reinterpret_cast<uintptr_t>(att)) & 15) == 0) {
         const float4* g4 = reinterpret_cast<const float4*>(grad);
         const float4* a4 = reinterpret_cast<const float4*>(att);
@@ -1037,13 +1034,18 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
             tph = reinterpret_cast<float2*>(bcur + L.tph);
         } else {
             stage_grow(k.grad_hist ? k.grad_hist + (size_t)p * nr : nullptr, k.geo.att, hs, nr, grow);
-            for (int t = lane; t < nt; t += 64)
+            const int ln = lane_opaque();
+            for (int t = ln; t < nt; t += 64)
                 tth[t] = make_float2(k.geo.sin_theta[(size_t)p * nt + t], k.geo.cos_theta[(size_t)p * nt + t]);
-            for (int t = lane; t < np_; t += 64)
+            for (int t = ln; t < np_; t += 64)
                 tph[t] = make_float2(k.geo.cos_phi[(size_t)p * np_ + t], k.geo.sin_phi[(size_t)p * np_ + t]);
         }
         owner[lane] = 0xFFFFFFFFu;
         const float px = k.geo.wall[3 * p], py = k.geo.wall[3 * p + 1], pz = k.geo.wall[3 * p + 2];
+        // per-pair row offset, recomputed per wall point (not hoisted as per-lane 64-bit pointers)
+        int gio = gi;
+        __asm__ __volatile__("" : "+v"(gio));
+        const size_t o = (size_t)p * k.g.ng + gio;
         // pair setup (lane = Gaussian gi at wall point p); the ray pass reads the pair table
         bool more = false;
         float M[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -1054,14 +1056,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
             Pair P;
             float mu_[3];
             load_rec(k.recs[gi], P, mu_);
-            if (CACHE) bx = k.cbox[(size_t)p * k.g.ng + gi];
+            if (CACHE) bx = k.cbox[o];
             if (CACHE && bx != 0u) {
                 // cached pair: u0 and the forward's albedo; no SH evaluation, no footprint (the
                 // recorded cells replace the quadric walk)
                 P.q[0] = px - mu[0]; P.q[1] = py - mu[1]; P.q[2] = pz - mu[2];
                 for (int r = 0; r < 3; ++r)
                     P.u0[r] = P.A[3 * r] * P.q[0] + P.A[3 * r + 1] * P.q[1] + P.A[3 * r + 2] * P.q[2];
-                P.rho = k.crho[(size_t)p * k.g.ng + gi];
+                P.rho = k.crho[o];
                 P.w = P.sigma * P.rho;
                 P.i0 = P.j0 = 0; P.i1 = P.j1 = 0;
                 for (int t = 0; t < 6; ++t) P.M[t] = 0.f;
@@ -1083,7 +1085,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
         int ci0 = 0, cj0 = 0, cw = 1;
         float rcw = 1.f;
         if (CACHE && active) {
-            const size_t o = (size_t)p * k.g.ng + gi;
             if (bx != 0u) {
                 const ulonglong2 cm = k.cmask[o];
                 cbits0 = more ? cm.x : 0ull;
@@ -1326,7 +1327,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
                 for (int cc = 0; cc < 3; ++cc) dA[3 * r + cc] += dU0p[r] * q[cc];
             for (int cc = 0; cc < 3; ++cc) dMu[cc] -= A[cc] * dU0p[0] + A[3 + cc] * dU0p[1] + A[6 + cc] * dU0p[2];
         }
-        if (active) k.drho[(size_t)p * k.g.ng + gi] = (wpair > 0.f && !(k.opt.flags & 64)) ? drho_pair : 0.f;
+        if (active) k.drho[o] = (wpair > 0.f && !(k.opt.flags & 64)) ? drho_pair : 0.f;
     }
     if (shr) {   // shared layout: every wave owns its Gaussians for the whole split
         if (active) {

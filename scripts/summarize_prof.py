@@ -8,7 +8,8 @@
                            GRBM/8).  Transcendentals issue for longer, so this is a lower bound.
   <tag>_sq_counters.csv    the raw SQ/GRBM rows of this library's kernels (LDS pass counters merged
                            into <tag>_valu.json per kernel)
-  <tag>_bench.json         the bench line of the same command
+  <tag>_bench.json         the bench line of the same command, its roofline.traffic and VALU figure
+                           restated from this run's passes
 
     python scripts/summarize_prof.py gpurun_out/prof_c3 r02_c3
 """
@@ -45,8 +46,6 @@ def main(src, tag):
     bench = open(os.path.join(src, "bench_default.log")).read().strip().splitlines()[-1]
     line = json.loads(bench)
     cutoff = line["config"]["cutoff"]
-    with open(os.path.join(out, f"{tag}_bench.json"), "w") as f:
-        f.write(bench + "\n")
     for f in glob.glob(os.path.join(src, "kt_*kernel_stats.csv")):
         shutil.copy(f, os.path.join(out, f"{tag}_kernel_stats.csv"))
     fetch = per_kernel(glob.glob(os.path.join(src, "fetch_*counter_collection.csv"))[0])
@@ -63,6 +62,13 @@ def main(src, tag):
     with open(os.path.join(out, f"{tag}_traffic.json"), "w") as f:
         json.dump({"source": f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE passes of bench.py ({tag})",
                    "cutoff": cutoff, "kernels": res}, f, indent=1)
+    # the bench line read the previously committed traffic/VALU profiles when it ran: restate its
+    # roofline.traffic from the passes of this same run
+    kl = line["roofline"]["kernel"].split("(", 1)[1].rstrip(")").split(" + ")
+    hits = [[v["hbm_bytes_per_launch"] for k, v in res.items() if sub in k] for sub in kl]
+    if all(hits):
+        line["roofline"]["traffic"] = sum(max(h) for h in hits)
+        line["roofline"]["traffic_source"] = f"profiles/{tag}_traffic.json"
     sqf = glob.glob(os.path.join(src, "sq_*counter_collection.csv"))
     if sqf:
         sq = per_kernel(sqf[0])
@@ -92,6 +98,11 @@ def main(src, tag):
             for row in rd:
                 if ours(row["Kernel_Name"]):
                     wr.writerow(row)
+        if dom and isinstance(line.get("compute"), dict):
+            line["compute"]["valu_issue_util"] = dom["valu_issue_util"]
+            line["compute"]["source"] = f"profiles/{tag}_valu.json"
+    with open(os.path.join(out, f"{tag}_bench.json"), "w") as f:
+        f.write(json.dumps(line) + "\n")
     for k, v in res.items():
         print(f"{v['hbm_bytes_per_launch'] / 1e6:10.2f} MB  {k[:90]}")
 
