@@ -61,6 +61,7 @@ constexpr int kCap = NLOSGR_MAX_PER_RAY;
 constexpr float kFullM2 = 180.0f;      // AABB selection: whole-ray support, pdf >= exp(-90)
 constexpr float kLog2e = 1.44269504088896341f;
 constexpr int kRowFloats = 32768;      // [ray][bin] float2 rows: 128 KB
+constexpr int kList = 32;              // live entries per wave list pass (8 floats each)
 
 struct TArgs {
     nlosgr_gaussians g;
@@ -95,7 +96,9 @@ struct TLayout {   // offsets in floats
         stage = rows + 2 * rt * nr;
         queue = stage + kWin * kStage;
         comb = queue + tb + kWin;          // queue capacity: one cull round + one window
-        misc = comb + kWin * 16;
+        // backward combine [kWin][16] / (rays phase) per-wave entry lists [waves][kList][8]
+        const int ncomb = kWin * 16 > (tb / 64) * kList * 8 ? kWin * 16 : (tb / 64) * kList * 8;
+        misc = comb + ncomb;
         total = misc + 256;
     }
 };
@@ -387,42 +390,55 @@ __global__ __launch_bounds__(tile_threads<BWD>()) void tile_kernel(TArgs k) {
                                     rho = o[19];
                                 }
                                 const bool live = kl <= kh;
-                                if (kDiag && k.diag) {
-                                    const unsigned long long lm = __builtin_amdgcn_ballot_w64(live);
-                                    if (tid == 0) nent += __popcll(lm);
-                                }
-                                const int lo = wave_min_i(live ? kl : nr);
-                                const int hi = wave_max_i(live ? kh : -1);
-                                if (lo > hi) continue;
-                                for (int c = lo >> 6; c <= (hi >> 6); ++c) {
-                                    unsigned long long cm =
-                                        __builtin_amdgcn_ballot_w64(live && kl <= c * 64 + 63 && kh >= c * 64);
-                                    if (kDiag && k.diag && tid == 0) { ++nchk; nec += __popcll(cm); }
-                                    if (!cm) continue;
-                                    const int kb = c * 64 + lane;
-                                    const float kf = (float)kb;
-                                    float accD = 0.f, accW = 0.f;
-                                    while (cm) {
-                                        const int s = __builtin_ctzll(cm);
-                                        cm &= cm - 1;
-                                        const float sks = rlf(ks, s), sga = rlf(ga, s), sal = rlf(al, s);
-                                        const float ssg = rlf(sg, s), srho = rlf(rho, s);
-                                        const int skl = rli(kl, s), skh = rli(kh, s);
-                                        const float tt = kf - sks;
-                                        const float pdf = fast_exp2(fmaf(sga, tt * tt, sal));
-                                        const float cv = (kb >= skl && kb <= skh) ? ssg * pdf : 0.f;
-                                        if (OCCL) {
-                                            accD += cv;
-                                            accW = fmaf(srho, 1.0f - fast_exp2(-cv * cdt * kLog2e), accW);
-                                        } else {
-                                            accW = fmaf(srho, cv, accW);
-                                        }
+                                const unsigned long long lm = __builtin_amdgcn_ballot_w64(live);
+                                if (kDiag && k.diag && tid == 0) nent += __popcll(lm);
+                                if (!lm) continue;
+                                // live entries (index order) go to this wave's LDS list, kList per pass;
+                                // lane = bin then reads them as broadcasts (uniform address)
+                                const int lrank = lanes_below(lm);
+                                float4* el = reinterpret_cast<float4*>(comb) + wave * kList * 2;
+                                for (int pb = 0; pb < __popcll(lm); pb += kList) {
+                                    const bool inp = live && lrank >= pb && lrank < pb + kList;
+                                    const unsigned long long pm = __builtin_amdgcn_ballot_w64(inp);
+                                    wave_sync();
+                                    if (inp) {
+                                        el[2 * (lrank - pb)] = make_float4(ks, ga, al, sg);
+                                        el[2 * (lrank - pb) + 1] =
+                                            make_float4(rho, __int_as_float(kl), __int_as_float(kh), 0.f);
                                     }
-                                    if (kb < nr) {
-                                        float2 v = rows[r * nr + kb];
-                                        v.x += accD;
-                                        v.y += accW;
-                                        rows[r * nr + kb] = v;
+                                    wave_sync();
+                                    const int lo = wave_min_i(inp ? kl : nr);
+                                    const int hi = wave_max_i(inp ? kh : -1);
+                                    for (int c = lo >> 6; c <= (hi >> 6); ++c) {
+                                        unsigned long long cm =
+                                            __builtin_amdgcn_ballot_w64(inp && kl <= c * 64 + 63 && kh >= c * 64);
+                                        if (kDiag && k.diag && tid == 0) { ++nchk; nec += __popcll(cm); }
+                                        if (!cm) continue;
+                                        const int kb = c * 64 + lane;
+                                        const float kf = (float)kb;
+                                        float accD = 0.f, accW = 0.f;
+                                        while (cm) {
+                                            const int s = __builtin_ctzll(cm);
+                                            cm &= cm - 1;
+                                            const int idx = __popcll(pm & ((1ull << s) - 1ull));
+                                            const float4 e0 = el[2 * idx], e1 = el[2 * idx + 1];
+                                            const int skl = __float_as_int(e1.y), skh = __float_as_int(e1.z);
+                                            const float tt = kf - e0.x;
+                                            const float pdf = fast_exp2(fmaf(e0.y, tt * tt, e0.z));
+                                            const float cv = (kb >= skl && kb <= skh) ? e0.w * pdf : 0.f;
+                                            if (OCCL) {
+                                                accD += cv;
+                                                accW = fmaf(e1.x, 1.0f - fast_exp2(-cv * cdt * kLog2e), accW);
+                                            } else {
+                                                accW = fmaf(e1.x, cv, accW);
+                                            }
+                                        }
+                                        if (kb < nr) {
+                                            float2 v = rows[r * nr + kb];
+                                            v.x += accD;
+                                            v.y += accW;
+                                            rows[r * nr + kb] = v;
+                                        }
                                     }
                                 }
                             }
