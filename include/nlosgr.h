@@ -76,8 +76,8 @@ enum {
 /* Gaussians: raw (pre-activation) parameters, exactly the reference GaussianModel tensors. */
 typedef struct {
     int32_t ng;               /* number of Gaussians */
-    int32_t k_feat;           /* feature row stride K >= (sh_degree+1)^2, K <= 16 */
-    int32_t sh_degree;        /* active SH degree, 0..3 */
+    int32_t k_feat;           /* feature row stride K >= (sh_degree+1)^2; K <= 25 (torch preset) / 16 (cuda) */
+    int32_t sh_degree;        /* active SH degree: 0..4 torch preset (sh_utils.py:57-112), 0..3 cuda preset */
     int32_t preset;           /* NLOSGR_PRESET_* */
     float scaling_modifier;   /* `mod` */
     const float* mu;          /* [ng,3]  _mu                                         */

@@ -21,7 +21,7 @@ inline int set_err(int code, const char* msg) {
 
 constexpr int kBlock = 256;
 constexpr int kWaves = kBlock / 64;
-constexpr int kMaxK = 16;
+constexpr int kMaxK = 16;      // SH coefficients up to degree 3 (cuda preset, path C / A kernels)
 constexpr int kNB = 64;          // Gaussians per backward workgroup
 constexpr float kPi = 3.14159265358979323846f;
 constexpr float kHalfLog2e = 0.72134752044448170368f;  // log2(e)/2

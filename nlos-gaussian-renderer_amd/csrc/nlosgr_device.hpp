@@ -14,6 +14,7 @@
 
 namespace nlosgr {
 
+constexpr int kMaxK4 = 25;     // SH degree 4 (torch preset, sh_utils.py:102-112): batched volume path only
 constexpr float kSH_C0 = 0.28209479177387814f;
 constexpr float kSH_C1 = 0.4886025119029199f;
 // 3DGS-signed constants (sh_utils.py:26-43)
@@ -22,6 +23,10 @@ constexpr float kC2_0 = 1.0925484305920792f, kC2_1 = -1.0925484305920792f, kC2_2
 constexpr float kC3_0 = -0.5900435899266435f, kC3_1 = 2.890611442640554f, kC3_2 = -0.4570457994644658f,
                 kC3_3 = 0.3731763325901154f, kC3_4 = -0.4570457994644658f, kC3_5 = 1.445305721320277f,
                 kC3_6 = -0.5900435899266435f;
+// degree 4 (sh_utils.py:44-54; torch preset only)
+constexpr float kC4_0 = 2.5033429417967046f, kC4_1 = -1.7701307697799304f, kC4_2 = 0.9461746957575601f,
+                kC4_3 = -0.6690465435572892f, kC4_4 = 0.10578554691520431f, kC4_5 = -0.6690465435572892f,
+                kC4_6 = 0.47308734787878004f, kC4_7 = -1.7701307697799304f, kC4_8 = 0.6258357354491761f;
 // unsigned constants (spherical_harmonics.cuh:20-54)
 constexpr float kU2_a = 1.0925484305920792f, kU2_b = 0.31539156525252005f, kU2_c = 0.5462742152960396f;
 constexpr float kU3_a = 0.5900435899266435f, kU3_b = 2.890611442640554f, kU3_c = 0.4570457994644658f,
@@ -65,6 +70,16 @@ __device__ __forceinline__ void sh_basis(int deg, float x, float y, float z, flo
         Y[14] = kU3_e * z * (xx - yy);
         Y[15] = kU3_a * x * (xx - 3.0f * yy);
     }
+    if (PRESET != NLOSGR_PRESET_TORCH || deg < 4) return;   // Y[16..24]: degree 4, torch preset only
+    Y[16] = kC4_0 * xy * (xx - yy);
+    Y[17] = kC4_1 * yz * (3.0f * xx - yy);
+    Y[18] = kC4_2 * xy * (7.0f * zz - 1.0f);
+    Y[19] = kC4_3 * yz * (7.0f * zz - 3.0f);
+    Y[20] = kC4_4 * (zz * (35.0f * zz - 30.0f) + 3.0f);
+    Y[21] = kC4_5 * xz * (7.0f * zz - 3.0f);
+    Y[22] = kC4_6 * (xx - yy) * (7.0f * zz - 1.0f);
+    Y[23] = kC4_7 * xz * (xx - 3.0f * yy);
+    Y[24] = kC4_8 * (xx * (xx - 3.0f * yy) - yy * (3.0f * xx - yy));
 }
 
 // sum_c f[c] Y_c(x,y,z) for c < (deg+1)^2, accumulated in c order without a Y[] array: the degree
@@ -78,12 +93,15 @@ __device__ __forceinline__ float sh_dot(int deg, float x, float y, float z, cons
     s += f[2] * (kSH_C1 * z);
     s += f[3] * (sg * kSH_C1 * x);
     if (deg < 2) return s;
-    float Y[16];
-    sh_basis<PRESET>(deg < 3 ? 2 : 3, x, y, z, Y);
+    float Y[kMaxK4];
+    sh_basis<PRESET>(deg < 3 ? 2 : deg, x, y, z, Y);
     s += f[4] * Y[4]; s += f[5] * Y[5]; s += f[6] * Y[6]; s += f[7] * Y[7]; s += f[8] * Y[8];
     if (deg < 3) return s;
 #pragma unroll
     for (int c = 9; c < 16; ++c) s += f[c] * Y[c];
+    if (PRESET != NLOSGR_PRESET_TORCH || deg < 4) return s;
+#pragma unroll
+    for (int c = 16; c < kMaxK4; ++c) s += f[c] * Y[c];
     return s;
 }
 
@@ -136,6 +154,33 @@ __device__ __forceinline__ void sh_grad_dir(int deg, float x, float y, float z, 
         gz += kU3_e * (xx - yy) * f[14];
         gx += kU3_a * (3.0f * xx - 3.0f * yy) * f[15]; gy += kU3_a * (-6.0f * x * y) * f[15];
     }
+    if (PRESET != NLOSGR_PRESET_TORCH || deg < 4) return;
+    // degree 4: partial derivatives of the sh_utils.py:102-112 polynomials (x, y, z independent)
+    const float xy = x * y, xz = x * z, yz = y * z;
+    // C4_0 xy(xx - yy)
+    gx += kC4_0 * y * (3.0f * xx - yy) * f[16];     gy += kC4_0 * x * (xx - 3.0f * yy) * f[16];
+    // C4_1 yz(3xx - yy)
+    gx += kC4_1 * 6.0f * xy * z * f[17];            gy += kC4_1 * z * (3.0f * xx - 3.0f * yy) * f[17];
+    gz += kC4_1 * y * (3.0f * xx - yy) * f[17];
+    // C4_2 xy(7zz - 1)
+    gx += kC4_2 * y * (7.0f * zz - 1.0f) * f[18];   gy += kC4_2 * x * (7.0f * zz - 1.0f) * f[18];
+    gz += kC4_2 * 14.0f * xy * z * f[18];
+    // C4_3 yz(7zz - 3)
+    gy += kC4_3 * z * (7.0f * zz - 3.0f) * f[19];   gz += kC4_3 * y * (21.0f * zz - 3.0f) * f[19];
+    // C4_4 (zz(35zz - 30) + 3)
+    gz += kC4_4 * z * (140.0f * zz - 60.0f) * f[20];
+    // C4_5 xz(7zz - 3)
+    gx += kC4_5 * z * (7.0f * zz - 3.0f) * f[21];   gz += kC4_5 * x * (21.0f * zz - 3.0f) * f[21];
+    // C4_6 (xx - yy)(7zz - 1)
+    gx += kC4_6 * 2.0f * x * (7.0f * zz - 1.0f) * f[22];  gy += kC4_6 * -2.0f * y * (7.0f * zz - 1.0f) * f[22];
+    gz += kC4_6 * 14.0f * z * (xx - yy) * f[22];
+    // C4_7 xz(xx - 3yy)
+    gx += kC4_7 * z * (3.0f * xx - 3.0f * yy) * f[23];    gy += kC4_7 * -6.0f * xy * z * f[23];
+    gz += kC4_7 * x * (xx - 3.0f * yy) * f[23];
+    // C4_8 (xx(xx - 3yy) - yy(3xx - yy)) = x^4 - 6 x^2 y^2 + y^4
+    gx += kC4_8 * (4.0f * xx * x - 12.0f * x * yy) * f[24];
+    gy += kC4_8 * (4.0f * yy * y - 12.0f * xx * y) * f[24];
+    (void)yz; (void)xz;
 }
 
 // Row-major R(q) for a unit quaternion (w,x,y,z): gaussian_utils.py:201-209 / cuda_utils.cuh:74-84.

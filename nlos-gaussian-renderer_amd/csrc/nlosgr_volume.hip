@@ -184,19 +184,20 @@ __device__ __forceinline__ void pair_setup(const KArgs& k, const float* f, const
 }
 
 // feature row -> registers (zero past k_feat)
+template <int KM>
 __device__ __forceinline__ void load_feat(const nlosgr_gaussians& g, int gi, float* f) {
     const float* src = g.features + (size_t)gi * g.k_feat;
-    if (g.k_feat == kMaxK && (reinterpret_cast<uintptr_t>(g.features) & 15) == 0) {
+    if (KM % 4 == 0 && g.k_feat == KM && (reinterpret_cast<uintptr_t>(g.features) & 15) == 0) {
         const float4* s4 = reinterpret_cast<const float4*>(src);
 #pragma unroll
-        for (int c = 0; c < kMaxK / 4; ++c) {
+        for (int c = 0; c < KM / 4; ++c) {
             const float4 v = s4[c];
             f[4 * c] = v.x; f[4 * c + 1] = v.y; f[4 * c + 2] = v.z; f[4 * c + 3] = v.w;
         }
         return;
     }
 #pragma unroll
-    for (int c = 0; c < kMaxK; ++c) f[c] = c < g.k_feat ? src[c] : 0.f;
+    for (int c = 0; c < KM; ++c) f[c] = c < g.k_feat ? src[c] : 0.f;
 }
 
 __device__ __forceinline__ float quadric(const float* M, float dx, float dy, float dz) {
@@ -742,10 +743,9 @@ __global__ __launch_bounds__(kBlock) void fwd_dense_kernel(KArgs k) {
         {
             const int gl = min(gi, k.g.ng - 1);
             const GaussRec rec = k.recs[gl];
-            float feat[kMaxK], mu[3];
-            load_feat(k.g, gl, feat);
+            float mu[3];
             load_rec(rec, P, mu);
-            pair_setup<PRESET, true>(k, feat, mu, px, py, pz, lin, 0.f, P);
+            pair_setup<PRESET, true>(k, k.g.features + (size_t)gl * k.g.k_feat, mu, px, py, pz, lin, 0.f, P);
             live = gi < g_hi && P.w > 0.f;
             lw = live ? flog2(P.w) : 0.f;
         }
@@ -822,7 +822,7 @@ __global__ __launch_bounds__(kBlock) void fwd_dense_kernel(KArgs k) {
 // Losers keep their result and retry next round.  No LDS float atomics, no pair/row tables.
 constexpr int kBSteps = 24;   // bins per lane per backward drain round
 constexpr int kBwdSlots = 13;   // per-Gaussian backward partial: dA[9], dMu[3], dsigma (stride 32 in HBM)
-constexpr int kShPart = 20;     // sh_kernel partial: dF[16], dMu[3], pad
+constexpr int kShPart = 28;     // sh_kernel partial: dF[KM <= 25], dMu[3] (at KM), pad
 
 // Two layouts.  Per-wave rows (default): each wave walks its own wall points and stages its own
 // upstream-gradient row and angle tables.  Shared rows (bwd_shared, long rows): the workgroup's 4
@@ -1363,7 +1363,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
 // dir = view direction of mu - p (preset convention; nlos_helpers / cuda_utils.cuh semantics as in
 // the forward's pair_setup).  One lane per Gaussian; drho rows [P][ng] are read coalesced.
 // ------------------------------------------------------------------------------------------
-template <int PRESET>
+// KM: coefficient registers (16 up to degree 3, 25 for degree 4); partial rows of kShPart floats
+template <int PRESET, int KM>
 __global__ __launch_bounds__(kBlock) void sh_kernel(KArgs k) {
     const int gi = k.g_lo + blockIdx.x * blockDim.x + threadIdx.x;
     if (gi >= k.g_hi) return;
@@ -1375,21 +1376,21 @@ __global__ __launch_bounds__(kBlock) void sh_kernel(KArgs k) {
     const int K = (deg + 1) * (deg + 1);
     const GaussRec rec = k.recs[gi];
     const float mu[3] = {rec.a.x, rec.a.y, rec.a.z};
-    float f[kMaxK];
-    load_feat(k.g, gi, f);
-    float dF[kMaxK], dMu[3] = {0.f, 0.f, 0.f};
+    float f[KM];
+    load_feat<KM>(k.g, gi, f);
+    float dF[KM], dMu[3] = {0.f, 0.f, 0.f};
 #pragma unroll
-    for (int c = 0; c < kMaxK; ++c) dF[c] = 0.f;
+    for (int c = 0; c < KM; ++c) dF[c] = 0.f;
     for (int p = pbeg; p < pend; ++p) {
         const float drho = k.drho[(size_t)p * k.g.ng + gi];
         if (drho == 0.f) continue;
         const float q[3] = {k.geo.wall[3 * p] - mu[0], k.geo.wall[3 * p + 1] - mu[1], k.geo.wall[3 * p + 2] - mu[2]};
         float dir[3], nrm;
         view_dir<PRESET>(-q[0], -q[1], -q[2], dir[0], dir[1], dir[2], nrm);
-        float Y[kMaxK];
+        float Y[KM];
         sh_basis<PRESET>(deg, dir[0], dir[1], dir[2], Y);
 #pragma unroll
-        for (int c = 0; c < kMaxK; ++c)
+        for (int c = 0; c < KM; ++c)
             if (c < K) dF[c] += drho * Y[c];
         float gx, gy, gz;
         sh_grad_dir<PRESET>(deg, dir[0], dir[1], dir[2], f, gx, gy, gz);
@@ -1399,28 +1400,28 @@ __global__ __launch_bounds__(kBlock) void sh_kernel(KArgs k) {
     }
     float* dst = k.shpart + ((size_t)split * k.g.ng + gi) * kShPart;
 #pragma unroll
-    for (int c = 0; c < kMaxK; ++c) dst[c] = dF[c];
-    dst[kMaxK] = dMu[0]; dst[kMaxK + 1] = dMu[1]; dst[kMaxK + 2] = dMu[2];
+    for (int c = 0; c < KM; ++c) dst[c] = dF[c];
+    dst[KM] = dMu[0]; dst[KM + 1] = dMu[1]; dst[KM + 2] = dMu[2];
 }
 
 // ------------------------------------------------------------------------------------------
 // finish: reduce the splits and chain dA / dsigma to the raw parameters
 // ------------------------------------------------------------------------------------------
-template <int PRESET>
+template <int PRESET, int KM>
 __global__ __launch_bounds__(kBlock) void finish_kernel(KArgs k, float* d_mu, float* d_scaling, float* d_rot,
                                                         float* d_opac, float* d_feat) {
     const int i = k.g_lo + blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= k.g_hi) return;
-    float acc[32];
-    for (int t = 0; t < 32; ++t) acc[t] = 0.f;
+    float acc[13 + KM];
+    for (int t = 0; t < 13 + KM; ++t) acc[t] = 0.f;
     for (int s = 0; s < k.nsplit; ++s) {
         const float* src = k.partial + ((size_t)s * k.g.ng + i) * 32;
         for (int t = 0; t < kBwdSlots; ++t) acc[t] += src[t];
     }
     for (int s = 0; s < k.nsh; ++s) {   // view-direction chain (sh_kernel)
         const float* src = k.shpart + ((size_t)s * k.g.ng + i) * kShPart;
-        for (int t = 0; t < kMaxK; ++t) acc[13 + t] += src[t];
-        for (int t = 0; t < 3; ++t) acc[9 + t] += src[kMaxK + t];
+        for (int t = 0; t < KM; ++t) acc[13 + t] += src[t];
+        for (int t = 0; t < 3; ++t) acc[9 + t] += src[KM + t];
     }
     chain_to_raw<PRESET>(k.g, i, acc, d_scaling, d_rot);
     d_mu[3 * i] = acc[9]; d_mu[3 * i + 1] = acc[10]; d_mu[3 * i + 2] = acc[11];
@@ -1429,7 +1430,7 @@ __global__ __launch_bounds__(kBlock) void finish_kernel(KArgs k, float* d_mu, fl
     const int kf = k.g.k_feat;
     const int K = (k.g.sh_degree + 1) * (k.g.sh_degree + 1);
 #pragma unroll
-    for (int c = 0; c < kMaxK; ++c)
+    for (int c = 0; c < KM; ++c)
         if (c < kf) d_feat[(size_t)i * kf + c] = c < K ? acc[13 + c] : 0.f;
 }
 
@@ -1453,10 +1454,15 @@ int validate(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr
     if (g->ng < 0) return set_err(NLOSGR_E_INVALID, "ng must be >= 0");
     if (g->preset != NLOSGR_PRESET_TORCH && g->preset != NLOSGR_PRESET_CUDA)
         return set_err(NLOSGR_E_INVALID, "unknown preset");
-    if (g->sh_degree < 0 || g->sh_degree > 3)
-        return set_err(NLOSGR_E_UNSUPPORTED, "active_sh_degree must be in [0, 3]");
-    if (g->k_feat < (g->sh_degree + 1) * (g->sh_degree + 1) || g->k_feat > kMaxK)
-        return set_err(NLOSGR_E_INVALID, "k_feat must satisfy (sh_degree+1)^2 <= k_feat <= 16");
+    // SH degree 4 exists in the torch preset only (sh_utils.py:102-112; spherical_harmonics.cuh stops at 3)
+    const int max_deg = g->preset == NLOSGR_PRESET_TORCH ? 4 : 3;
+    if (g->sh_degree < 0 || g->sh_degree > max_deg)
+        return set_err(NLOSGR_E_UNSUPPORTED, g->preset == NLOSGR_PRESET_TORCH ? "active_sh_degree must be in [0, 4]"
+                                                                              : "active_sh_degree must be in [0, 3] (cuda preset)");
+    const int max_k = g->preset == NLOSGR_PRESET_TORCH ? kMaxK4 : kMaxK;
+    if (g->k_feat < (g->sh_degree + 1) * (g->sh_degree + 1) || g->k_feat > max_k)
+        return set_err(NLOSGR_E_INVALID, g->preset == NLOSGR_PRESET_TORCH ? "k_feat must satisfy (sh_degree+1)^2 <= k_feat <= 25"
+                                                                           : "k_feat must satisfy (sh_degree+1)^2 <= k_feat <= 16");
     if (opt->mode != NLOSGR_MODE_NOOCL && opt->mode != NLOSGR_MODE_NETF && opt->mode != NLOSGR_MODE_BININT &&
         opt->mode != NLOSGR_MODE_OCCL)
         return set_err(NLOSGR_E_INVALID, "unknown mode");
@@ -1761,22 +1767,27 @@ int nlosgr_render_bwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo, con
         }
         HIPCHK(hipGetLastError());
         const dim3 shgrid((ka.g_hi - ka.g_lo + kBlock - 1) / kBlock, ka.nsh);
-        if (g->preset == NLOSGR_PRESET_TORCH)
-            hipLaunchKernelGGL(sh_kernel<NLOSGR_PRESET_TORCH>, shgrid, dim3(kBlock), 0, s, ka);
+        if (g->preset == NLOSGR_PRESET_TORCH && g->sh_degree == 4)
+            hipLaunchKernelGGL((sh_kernel<NLOSGR_PRESET_TORCH, kMaxK4>), shgrid, dim3(kBlock), 0, s, ka);
+        else if (g->preset == NLOSGR_PRESET_TORCH)
+            hipLaunchKernelGGL((sh_kernel<NLOSGR_PRESET_TORCH, kMaxK>), shgrid, dim3(kBlock), 0, s, ka);
         else
-            hipLaunchKernelGGL(sh_kernel<NLOSGR_PRESET_CUDA>, shgrid, dim3(kBlock), 0, s, ka);
+            hipLaunchKernelGGL((sh_kernel<NLOSGR_PRESET_CUDA, kMaxK>), shgrid, dim3(kBlock), 0, s, ka);
         HIPCHK(hipGetLastError());
     } else {
         HIPCHK(hipMemsetAsync(ka.partial, 0, (size_t)ka.nsplit * g->ng * 32 * sizeof(float), s));
         ka.nsh = 0;
     }
     const int nb = (ka.g_hi - ka.g_lo + kBlock - 1) / kBlock;
-    if (g->preset == NLOSGR_PRESET_TORCH)
-        hipLaunchKernelGGL(finish_kernel<NLOSGR_PRESET_TORCH>, dim3(nb), dim3(kBlock), 0, s, ka, d_mu, d_scaling,
-                           d_rotation, d_opacity, d_features);
+    if (g->preset == NLOSGR_PRESET_TORCH && g->sh_degree == 4)
+        hipLaunchKernelGGL((finish_kernel<NLOSGR_PRESET_TORCH, kMaxK4>), dim3(nb), dim3(kBlock), 0, s, ka, d_mu,
+                           d_scaling, d_rotation, d_opacity, d_features);
+    else if (g->preset == NLOSGR_PRESET_TORCH)
+        hipLaunchKernelGGL((finish_kernel<NLOSGR_PRESET_TORCH, kMaxK>), dim3(nb), dim3(kBlock), 0, s, ka, d_mu,
+                           d_scaling, d_rotation, d_opacity, d_features);
     else
-        hipLaunchKernelGGL(finish_kernel<NLOSGR_PRESET_CUDA>, dim3(nb), dim3(kBlock), 0, s, ka, d_mu, d_scaling,
-                           d_rotation, d_opacity, d_features);
+        hipLaunchKernelGGL((finish_kernel<NLOSGR_PRESET_CUDA, kMaxK>), dim3(nb), dim3(kBlock), 0, s, ka, d_mu,
+                           d_scaling, d_rotation, d_opacity, d_features);
     HIPCHK(hipGetLastError());
     return NLOSGR_OK;
 }

@@ -27,6 +27,9 @@ C2 = [1.0925484305920792, -1.0925484305920792, 0.31539156525252005, -1.092548430
       0.5462742152960396]
 C3 = [-0.5900435899266435, 2.890611442640554, -0.4570457994644658, 0.3731763325901154,
       -0.4570457994644658, 1.445305721320277, -0.5900435899266435]
+C4 = [2.5033429417967046, -1.7701307697799304, 0.9461746957575601, -0.6690465435572892,
+      0.10578554691520431, -0.6690465435572892, 0.47308734787878004, -1.7701307697799304,
+      0.6258357354491761]   # sh_utils.py:44-54
 
 
 # --------------------------------------------------------------------------------------------
@@ -116,8 +119,8 @@ def quat_to_rotmat_cuda(q):
 
 
 def eval_sh(deg, sh, dirs):
-    """sh_utils.py:57-112 (3DGS sign convention), degrees 0..3."""
-    assert 0 <= deg <= 3
+    """sh_utils.py:57-112 (3DGS sign convention), degrees 0..4."""
+    assert 0 <= deg <= 4
     result = C0 * sh[..., 0]
     if deg > 0:
         x, y, z = dirs[..., 0:1], dirs[..., 1:2], dirs[..., 2:3]
@@ -136,6 +139,16 @@ def eval_sh(deg, sh, dirs):
                           + C3[4] * x * (4 * zz - xx - yy) * sh[..., 13]
                           + C3[5] * z * (xx - yy) * sh[..., 14]
                           + C3[6] * x * (xx - 3 * yy) * sh[..., 15])
+                if deg > 3:   # sh_utils.py:102-112
+                    result = (result + C4[0] * xy * (xx - yy) * sh[..., 16]
+                              + C4[1] * yz * (3 * xx - yy) * sh[..., 17]
+                              + C4[2] * xy * (7 * zz - 1) * sh[..., 18]
+                              + C4[3] * yz * (7 * zz - 3) * sh[..., 19]
+                              + C4[4] * (zz * (35 * zz - 30) + 3) * sh[..., 20]
+                              + C4[5] * xz * (7 * zz - 3) * sh[..., 21]
+                              + C4[6] * (xx - yy) * (7 * zz - 1) * sh[..., 22]
+                              + C4[7] * xz * (xx - 3 * yy) * sh[..., 23]
+                              + C4[8] * (xx * (xx - 3 * yy) - yy * (3 * xx - yy)) * sh[..., 24])
     return result
 
 

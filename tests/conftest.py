@@ -13,7 +13,8 @@ for p in (ROOT, PKG):
 
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 CASES = ["noocl_g16_s4_r16_d0", "noocl_g64_s8_r32_d3", "netf_g64_s4_r16_d3",
-         "noocl_g256_s8_r64_d3", "netf_g32_s8_r64_d1", "noocl_g16_s5_r24_d2"]
+         "noocl_g256_s8_r64_d3", "netf_g32_s8_r64_d1", "noocl_g16_s5_r24_d2",
+         "noocl_g32_s4_r16_d4", "netf_g32_s4_r16_d4"]   # SH degree 4: torch preset
 
 
 def pytest_configure(config):

@@ -163,6 +163,12 @@ def run_case(name, ng, ns, nr, deg, nwall, occlusion, seed, out):
     print(name, "hist max", np.abs(rec["hist"]).max(), "loss", losses)
 
 
+CASES = {
+    "noocl_g32_s4_r16_d4": dict(ng=32, ns=4, nr=16, deg=4, nwall=2, occlusion=False, seed=70),
+    "netf_g32_s4_r16_d4": dict(ng=32, ns=4, nr=16, deg=4, nwall=1, occlusion=True, seed=80),
+}
+
+
 def run_units(out):
     gu, shu, GaussianModel, H, Config = import_reference()
     g = torch.Generator().manual_seed(7)
@@ -196,6 +202,12 @@ def run_units(out):
 if __name__ == "__main__":
     torch.set_num_threads(min(8, os.cpu_count() or 1))
     out = HERE
+    only = sys.argv[1:]   # optional case names: regenerate just those
+    if only:
+        for name in only:
+            kw = dict(CASES[name])
+            run_case(name, out=out, **kw)
+        sys.exit(0)
     run_units(out)
     run_case("noocl_g16_s4_r16_d0", ng=16, ns=4, nr=16, deg=0, nwall=1, occlusion=False, seed=10, out=out)
     run_case("noocl_g64_s8_r32_d3", ng=64, ns=8, nr=32, deg=3, nwall=2, occlusion=False, seed=20, out=out)
@@ -203,3 +215,6 @@ if __name__ == "__main__":
     run_case("noocl_g256_s8_r64_d3", ng=256, ns=8, nr=64, deg=3, nwall=1, occlusion=False, seed=40, out=out)
     run_case("netf_g32_s8_r64_d1", ng=32, ns=8, nr=64, deg=1, nwall=1, occlusion=True, seed=50, out=out)
     run_case("noocl_g16_s5_r24_d2", ng=16, ns=5, nr=24, deg=2, nwall=3, occlusion=False, seed=60, out=out)
+    # SH degree 4 (sh_utils.py:102-112; torch preset only)
+    run_case("noocl_g32_s4_r16_d4", ng=32, ns=4, nr=16, deg=4, nwall=2, occlusion=False, seed=70, out=out)
+    run_case("netf_g32_s4_r16_d4", ng=32, ns=4, nr=16, deg=4, nwall=1, occlusion=True, seed=80, out=out)

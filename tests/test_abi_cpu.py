@@ -31,11 +31,17 @@ def test_validation_errors_without_gpu():
     """Argument validation runs on the host and reports through nlosgr_last_error."""
     from nlosgr import _lib
     lib = _lib.load()
-    g = _lib.Gaussians(10, 16, 4, 0, 1.0, None, None, None, None, None)       # degree 4: unsupported
+    g = _lib.Gaussians(10, 25, 5, 0, 1.0, None, None, None, None, None)       # degree 5: unsupported
     geo = _lib.Geometry(1, 4, 4, 8, None, None, None, None, None, None, None, None, None)
     opt = _lib.Options(0, 0.0, 1.0, 1.0, 0, 0)
     rc = lib.nlosgr_render_fwd(g, geo, opt, None, None, None, None)
     assert rc == 3 and b"active_sh_degree" in lib.nlosgr_last_error()
+    g = _lib.Gaussians(10, 25, 4, 1, 1.0, None, None, None, None, None)       # degree 4: torch preset only
+    rc = lib.nlosgr_render_fwd(g, geo, opt, None, None, None, None)
+    assert rc == 3 and b"cuda preset" in lib.nlosgr_last_error()
+    g = _lib.Gaussians(10, 16, 4, 0, 1.0, None, None, None, None, None)       # degree 4 needs 25 coefficients
+    rc = lib.nlosgr_render_fwd(g, geo, opt, None, None, None, None)
+    assert rc == 1 and b"k_feat" in lib.nlosgr_last_error()
     g = _lib.Gaussians(10, 4, 1, 7, 1.0, None, None, None, None, None)        # bad preset
     assert lib.nlosgr_render_fwd(g, geo, opt, None, None, None, None) == 1
     g = _lib.Gaussians(10, 4, 1, 0, 1.0, None, None, None, None, None)        # null param pointers

@@ -86,11 +86,23 @@ def _oracle_volume(d_params, walls, box, Y, ns, start, end, c, deltaT, preset, m
 def test_volume_vs_oracle(preset, mode, cutoff):
     """Batched volume render (several wall points in one launch) + grads vs the oracle (same
     Mahalanobis support mask when cutoff > 0)."""
+    _volume_vs_oracle(preset, mode, cutoff, 3)
+
+
+@pytest.mark.parametrize("mode", ["noocl", "netf"])
+@pytest.mark.parametrize("cutoff", [0.0, 3.0])
+def test_volume_vs_oracle_sh_degree4(mode, cutoff):
+    """SH degree 4 (25 coefficients; sh_utils.py:102-112, torch preset): albedo, feature gradients
+    and the view-direction chain into mu vs the oracle (itself pinned to the deg-4 golden cases)."""
+    _volume_vs_oracle("torch", mode, cutoff, 4)
+
+
+def _volume_vs_oracle(preset, mode, cutoff, deg):
     from nlosgr import GaussianParams, features_flat
     from nlosgr.geometry import build_geometry, relay_wall_grid, volume_box_point
     from nlosgr.render import RenderConfig, render
     dev = torch.device("cuda:0")
-    ng, deg, ns, T = 48, 3, 6, 40
+    ng, ns, T = 48, 6, 40
     c, deltaT = 1.0, 1.28 / T
     start, end = T // 8, T // 8 + T
     model = GaussianParams.synthetic(ng, deg, preset=preset, device=dev, seed=3)

@@ -15,7 +15,7 @@ def _params(d):
 def test_units_sh_rotation_pdf():
     u = load_case("units")
     dirs = torch.from_numpy(u["sh_dirs"])
-    for deg in range(4):
+    for deg in range(5):
         out = R.eval_sh(deg, torch.from_numpy(u[f"sh{deg}_coef"]), dirs)
         np.testing.assert_allclose(out.numpy(), u[f"sh{deg}_out"], rtol=1e-6, atol=1e-6)
     Rm = R.build_rotation(torch.from_numpy(u["rot_q"]))
