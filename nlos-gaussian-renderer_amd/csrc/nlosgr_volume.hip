@@ -554,35 +554,37 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
                 // kSteps bins from the even bin at or below pos: one ds_read_b64 + ds_write_b64 per 2
                 // bins, values by the exp2 recurrence (see kRecurrence).  Slots before pos (first round
                 // of a segment only) add 0 and do not advance the recurrence, which starts at pos.
+                // The whole round is one EXEC region of the winners (losers take no LDS bank and no
+                // per-step mask switching).
                 const int o = d.pos & (VW - 1);
                 const int lim = remw + o;   // slot j is in the segment iff o <= j < lim
-                float cur = fast_exp2(fmaf(d.ga, t * t, d.al));
-                float q = fast_exp2(d.ga * fmaf(2.f, t, 1.f));
-                const float cc = fast_exp2(2.f * d.ga);
-                float2* hb2 = reinterpret_cast<float2*>(hb);
+                if (win) {
+                    float cur = fast_exp2(fmaf(d.ga, t * t, d.al));
+                    float q = fast_exp2(d.ga * fmaf(2.f, t, 1.f));
+                    const float cc = fast_exp2(2.f * d.ga);
+                    float2* hb2 = reinterpret_cast<float2*>(hb);
 #pragma unroll
-                for (int kv = 0; kv < kSteps / VW; ++kv) {
-                    float v[VW];
+                    for (int kv = 0; kv < kSteps / VW; ++kv) {
+                        float v[VW];
 #pragma unroll
-                    for (int jj = 0; jj < VW; ++jj) {
-                        const int j = VW * kv + jj;
-                        if (kv == 0) {
-                            const bool st = jj >= o;
-                            v[jj] = (st && j < lim) ? cur : 0.f;
-                            cur = st ? cur * q : cur;
-                            q = st ? q * cc : q;
-                        } else {
-                            v[jj] = j < lim ? cur : 0.f;
-                            cur *= q;
-                            q *= cc;
+                        for (int jj = 0; jj < VW; ++jj) {
+                            const int j = VW * kv + jj;
+                            if (kv == 0) {
+                                const bool st = jj >= o;
+                                v[jj] = (st && j < lim) ? cur : 0.f;
+                                cur = st ? cur * q : cur;
+                                q = st ? q * cc : q;
+                            } else {
+                                v[jj] = j < lim ? cur : 0.f;
+                                cur *= q;
+                                q *= cc;
+                            }
                         }
-                    }
-                    if (win) {   // losers stay out of the LDS ops (EXEC-masked lanes take no bank)
                         float2 x = hb2[kv];
                         x.x += v[0]; x.y += v[1];
                         hb2[kv] = x;
+                        compiler_fence();
                     }
-                    compiler_fence();
                 }
                 t += (float)(kSteps - o);
             } else
