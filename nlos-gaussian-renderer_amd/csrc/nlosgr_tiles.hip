@@ -62,6 +62,7 @@ constexpr float kFullM2 = 180.0f;      // AABB selection: whole-ray support, pdf
 constexpr float kLog2e = 1.44269504088896341f;
 constexpr int kRowFloats = 32768;      // [ray][bin] float2 rows: 128 KB
 constexpr int kList = 32;              // live entries per wave list pass (8 floats each)
+constexpr int kSlot = 6;               // backward pair slot: m0 m1 m2 dsigma drho | key
 
 struct TArgs {
     nlosgr_gaussians g;
@@ -91,15 +92,18 @@ __host__ __device__ inline int tile_rays(int nr) {
 
 struct TLayout {   // offsets in floats
     int rows, stage, queue, comb, misc, total;
-    __host__ __device__ TLayout(int rt, int nr, int tb) {
+    __host__ __device__ TLayout(int rt, int nr, int tb, bool bwd) {
         rows = 0;
         stage = rows + 2 * rt * nr;
         queue = stage + kWin * kStage;
-        comb = queue + tb + kWin;          // queue capacity: one cull round + one window
-        // backward combine [kWin][16] / (rays phase) per-wave entry lists [waves][kList][8]
-        const int ncomb = kWin * 16 > (tb / 64) * kList * 8 ? kWin * 16 : (tb / 64) * kList * 8;
-        misc = comb + ncomb;
-        total = misc + 256;
+        misc = queue + tb + kWin;          // queue capacity: one cull round + one window
+        comb = misc + 256;
+        // shared scratch: backward combine [kWin][16] / (rays phase) per-wave entry lists
+        // [waves][kList][8] / (backward pairs) per-wave pair slots [waves][64][kSlot]
+        int ncomb = kWin * 16;
+        if ((tb / 64) * kList * 8 > ncomb) ncomb = (tb / 64) * kList * 8;
+        if (bwd && (tb / 64) * 64 * kSlot > ncomb) ncomb = (tb / 64) * 64 * kSlot;
+        total = comb + ncomb;
     }
 };
 
@@ -198,7 +202,7 @@ __global__ __launch_bounds__(tile_threads<BWD>()) void tile_kernel(TArgs k) {
     constexpr int kTW = kTB / 64;
     extern __shared__ __align__(16) float sm[];
     const int nr = k.geo.nr, nt = k.geo.nt, np_ = k.geo.np;
-    const TLayout L(k.rt, nr, kTB);
+    const TLayout L(k.rt, nr, kTB, BWD);
     float2* rows = reinterpret_cast<float2*>(sm + L.rows);
     float* stage = sm + L.stage;
     int* queue = reinterpret_cast<int*>(sm + L.queue);
@@ -473,10 +477,22 @@ __global__ __launch_bounds__(tile_threads<BWD>()) void tile_kernel(TArgs k) {
                         float dA[9] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
                         float gU[3] = {0.f, 0.f, 0.f};
                         float dsig = 0.f, drho = 0.f;
-                        for (int r = rg; r < RT; r += 4) {
+                        // rays r = rg + 4 (4 rb + kk): blocks of four per ray group
+                        for (int rb = 0; 16 * rb < RT; ++rb) {
+                        // (1) lane = entry: which of the block's 4 rays select the entry and cross its
+                        //     support -> one live mask per ray
+                        unsigned long long live_m[4];
+                        float rdx[4], rdy[4], rdz[4];   // ray directions (wave-uniform)
+#pragma unroll
+                        for (int kk = 0; kk < 4; ++kk) {
+                            live_m[kk] = 0ull;
+                            rdx[kk] = rdy[kk] = rdz[kk] = 0.f;
+                            const int r = rg + 4 * (4 * rb + kk);
+                            if (r >= RT) continue;
                             const int i = ti0 + r / k.tj, j = tj0 + r % k.tj;
                             if (i >= nt || j >= np_) continue;
                             const float dx = sth[i] * cph[j], dy = sth[i] * sph[j], dz = cth[i];
+                            rdx[kk] = dx; rdy[kk] = dy; rdz[kk] = dz;
                             bool sel = valid;
                             if (SEL == NLOSGR_SELECT_AABB) {
                                 sel = valid && slab_hit(sel6, px, py, pz, 1.0f / (dx + 1e-8f), 1.0f / (dy + 1e-8f),
@@ -487,59 +503,124 @@ __global__ __launch_bounds__(tile_threads<BWD>()) void tile_kernel(TArgs k) {
                             } else if (!DENSE && valid) {
                                 sel = quadric(sel6, dx, dy, dz) >= 0.f;
                             }
-                            if (!sel) continue;
-                            float v[3];
-                            for (int x = 0; x < 3; ++x) v[x] = A[3 * x] * dx + A[3 * x + 1] * dy + A[3 * x + 2] * dz;
-                            const float a = v[0] * v[0] + v[1] * v[1] + v[2] * v[2];
-                            const float b = u0[0] * v[0] + u0[1] * v[1] + u0[2] * v[2];
-                            const float ia = 1.0f / a;
-                            const float ts = -b * ia;
-                            const float zs[3] = {u0[0] + ts * v[0], u0[1] + ts * v[1], u0[2] + ts * v[2]};
-                            const float m2min = zs[0] * zs[0] + zs[1] * zs[1] + zs[2] * zs[2];
-                            const float ks = (ts - r0) * inv_dr;
-                            int kl = 0, kh = nr - 1;
-                            if (!DENSE) {
-                                if (!(m2min <= mc2)) continue;
-                                const float hk = sqrtf((mc2 - m2min) * ia) * inv_dr;
-                                kl = fidx(ceilf(ks - hk), 0, nr);
-                                kh = fidx(floorf(ks + hk), -1, nr - 1);
-                            }
-                            const float ga = -0.5f * kLog2e * a * dr * dr;
-                            const float al = -0.5f * kLog2e * m2min;
-                            float m0 = 0.f, m1 = 0.f, m2 = 0.f;
-                            const float2* row = rows + r * nr;
-                            for (int kb = kl; kb <= kh; ++kb) {
-                                const float tt = (float)kb - ks;
-                                const float pdf = fast_exp2(fmaf(ga, tt * tt, al));
-                                const float cv = sg * pdf;
-                                const float2 ab = row[kb];
-                                float dc;
-                                if (OCCL) {
-                                    const float ex = fast_exp2(-cv * cdt * kLog2e);
-                                    dc = fmaf(ab.x * rho * cdt, ex, ab.y);
-                                    drho = fmaf(ab.x, 1.0f - ex, drho);
-                                } else {
-                                    dc = ab.x * rho;
-                                    drho = fmaf(ab.x, cv, drho);
+                            bool live = false;
+                            if (sel) {
+                                float v[3];
+                                for (int x = 0; x < 3; ++x) v[x] = A[3 * x] * dx + A[3 * x + 1] * dy + A[3 * x + 2] * dz;
+                                const float a = v[0] * v[0] + v[1] * v[1] + v[2] * v[2];
+                                const float b = u0[0] * v[0] + u0[1] * v[1] + u0[2] * v[2];
+                                const float ia = 1.0f / a;
+                                const float ts = -b * ia;
+                                const float z0 = u0[0] + ts * v[0], z1 = u0[1] + ts * v[1], z2 = u0[2] + ts * v[2];
+                                const float m2min = z0 * z0 + z1 * z1 + z2 * z2;
+                                if (DENSE) {
+                                    live = true;
+                                } else if (m2min <= mc2) {
+                                    const float ks = (ts - r0) * inv_dr;
+                                    const float hk = sqrtf((mc2 - m2min) * ia) * inv_dr;
+                                    live = fidx(ceilf(ks - hk), 0, nr) <= fidx(floorf(ks + hk), -1, nr - 1);
                                 }
-                                dsig = fmaf(dc, pdf, dsig);
-                                const float G = dc * cv;
-                                m0 += G;
-                                m1 = fmaf(G, tt, m1);
-                                m2 = fmaf(G * tt, tt, m2);
                             }
-                            // pdf = exp(-|z|^2 / 2), z_k = zs + tau_k v, tau = (k - ks) dr:
-                            // dL/du0 = -(zs M0 + v M1), dL/dv = -(zs (M1 + ts M0) + v (M2 + ts M1))
-                            const float M0 = m0, M1 = m1 * dr, M2 = m2 * dr * dr;
-                            const float d3[3] = {dx, dy, dz};
-                            for (int x = 0; x < 3; ++x) {
-                                const float gu = -(zs[x] * M0 + v[x] * M1);
-                                const float gv = -(zs[x] * (M1 + ts * M0) + v[x] * (M2 + ts * M1));
-                                gU[x] += gu;
-                                for (int c = 0; c < 3; ++c) dA[3 * x + c] = fmaf(gv, d3[c], dA[3 * x + c]);
+                            live_m[kk] = __builtin_amdgcn_ballot_w64(live);
+                        }
+                        int lbase[5];
+                        lbase[0] = 0;
+#pragma unroll
+                        for (int kk = 0; kk < 4; ++kk) lbase[kk + 1] = lbase[kk] + __popcll(live_m[kk]);
+                        float* slots = comb + wave * 64 * kSlot;
+                        // (2) the live (entry, ray) pairs, 64 per pass, one per lane: lane = pair walks
+                        //     the pair's in-support bins and leaves its moments in the wave's slots;
+                        // (3) lane = entry folds its pairs in ray order (fixed order: deterministic)
+                        for (int pb = 0; pb < lbase[4]; pb += 64) {
+                            wave_sync();
+#pragma unroll
+                            for (int kk = 0; kk < 4; ++kk) {
+                                const int idx = lbase[kk] + lanes_below(live_m[kk]) - pb;
+                                if (((live_m[kk] >> lane) & 1ull) && idx >= 0 && idx < 64)
+                                    slots[idx * kSlot + 5] = __int_as_float((kk << 8) | lane);
+                            }
+                            wave_sync();
+                            if (pb + lane < lbase[4]) {
+                                const int key = __float_as_int(slots[lane * kSlot + 5]);
+                                const int kk = key >> 8, ew = half * 64 + (key & 255);
+                                const float dx = kk == 0 ? rdx[0] : kk == 1 ? rdx[1] : kk == 2 ? rdx[2] : rdx[3];
+                                const float dy = kk == 0 ? rdy[0] : kk == 1 ? rdy[1] : kk == 2 ? rdy[2] : rdy[3];
+                                const float dz = kk == 0 ? rdz[0] : kk == 1 ? rdz[1] : kk == 2 ? rdz[2] : rdz[3];
+                                const float* ow = stage + ew * kStage;
+                                float v[3];
+                                for (int x = 0; x < 3; ++x) v[x] = ow[3 * x] * dx + ow[3 * x + 1] * dy + ow[3 * x + 2] * dz;
+                                const float wu0 = ow[9], wu1 = ow[10], wu2 = ow[11], wsg = ow[18], wrho = ow[19];
+                                const float a = v[0] * v[0] + v[1] * v[1] + v[2] * v[2];
+                                const float b = wu0 * v[0] + wu1 * v[1] + wu2 * v[2];
+                                const float ia = 1.0f / a;
+                                const float ts = -b * ia;
+                                const float z0 = wu0 + ts * v[0], z1 = wu1 + ts * v[1], z2 = wu2 + ts * v[2];
+                                const float m2min = z0 * z0 + z1 * z1 + z2 * z2;
+                                const float ks = (ts - r0) * inv_dr;
+                                int kl = 0, kh = nr - 1;
+                                if (!DENSE) {
+                                    const float hk = sqrtf(fmaxf(mc2 - m2min, 0.f) * ia) * inv_dr;
+                                    kl = fidx(ceilf(ks - hk), 0, nr);
+                                    kh = fidx(floorf(ks + hk), -1, nr - 1);
+                                }
+                                const float ga = -0.5f * kLog2e * a * dr * dr;
+                                const float al = -0.5f * kLog2e * m2min;
+                                float m0 = 0.f, m1 = 0.f, m2 = 0.f, ps = 0.f, pr = 0.f;
+                                const float2* row = rows + (rg + 4 * (4 * rb + kk)) * nr;
+                                for (int kb = kl; kb <= kh; ++kb) {
+                                    const float tt = (float)kb - ks;
+                                    const float pdf = fast_exp2(fmaf(ga, tt * tt, al));
+                                    const float cv = wsg * pdf;
+                                    const float2 ab = row[kb];
+                                    float dc;
+                                    if (OCCL) {
+                                        const float ex = fast_exp2(-cv * cdt * kLog2e);
+                                        dc = fmaf(ab.x * wrho * cdt, ex, ab.y);
+                                        pr = fmaf(ab.x, 1.0f - ex, pr);
+                                    } else {
+                                        dc = ab.x * wrho;
+                                        pr = fmaf(ab.x, cv, pr);
+                                    }
+                                    ps = fmaf(dc, pdf, ps);
+                                    const float G = dc * cv;
+                                    m0 += G;
+                                    m1 = fmaf(G, tt, m1);
+                                    m2 = fmaf(G * tt, tt, m2);
+                                }
+                                float* sl = slots + lane * kSlot;
+                                sl[0] = m0; sl[1] = m1; sl[2] = m2; sl[3] = ps; sl[4] = pr;
+                            }
+                            wave_sync();
+#pragma unroll
+                            for (int kk = 0; kk < 4; ++kk) {
+                                const int idx = lbase[kk] + lanes_below(live_m[kk]) - pb;
+                                if (!(((live_m[kk] >> lane) & 1ull) && idx >= 0 && idx < 64)) continue;
+                                const float* sl = slots + idx * kSlot;
+                                const float dx = rdx[kk], dy = rdy[kk], dz = rdz[kk];
+                                float v[3];
+                                for (int x = 0; x < 3; ++x) v[x] = A[3 * x] * dx + A[3 * x + 1] * dy + A[3 * x + 2] * dz;
+                                const float a = v[0] * v[0] + v[1] * v[1] + v[2] * v[2];
+                                const float b = u0[0] * v[0] + u0[1] * v[1] + u0[2] * v[2];
+                                const float ts = -b * (1.0f / a);
+                                const float zs[3] = {u0[0] + ts * v[0], u0[1] + ts * v[1], u0[2] + ts * v[2]};
+                                dsig += sl[3];
+                                drho += sl[4];
+                                // pdf = exp(-|z|^2 / 2), z_k = zs + tau_k v, tau = (k - ks) dr:
+                                // dL/du0 = -(zs M0 + v M1), dL/dv = -(zs (M1 + ts M0) + v (M2 + ts M1))
+                                const float M0 = sl[0], M1 = sl[1] * dr, M2 = sl[2] * dr * dr;
+                                const float d3[3] = {dx, dy, dz};
+                                for (int x = 0; x < 3; ++x) {
+                                    const float gu = -(zs[x] * M0 + v[x] * M1);
+                                    const float gv = -(zs[x] * (M1 + ts * M0) + v[x] * (M2 + ts * M1));
+                                    gU[x] += gu;
+                                    for (int c = 0; c < 3; ++c) dA[3 * x + c] = fmaf(gv, d3[c], dA[3 * x + c]);
+                                }
                             }
                         }
-                        // combine the four ray groups per entry in order rg = 0..3
+                        }
+                        // combine the four ray groups per entry in order rg = 0..3 (comb overlaps the
+                        // pair slots: every wave must be done with them first)
+                        __syncthreads();
                         for (int step = 0; step < 4; ++step) {
                             if (rg == step && valid) {
                                 float* cb = comb + e * 16;
@@ -862,7 +943,7 @@ int tiles_validate(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const 
     if (opt->selection != NLOSGR_SELECT_SUPPORT && opt->selection != NLOSGR_SELECT_AABB)
         return set_err(NLOSGR_E_INVALID, "unknown selection");
     if (geo->nr > 4096) return set_err(NLOSGR_E_UNSUPPORTED, "occl / AABB engine: nr <= 4096");
-    if ((size_t)TLayout(tile_rays(geo->nr), geo->nr, tile_threads<false>()).total * 4 > 160 * 1024)
+    if ((size_t)TLayout(tile_rays(geo->nr), geo->nr, tile_threads<false>(), false).total * 4 > 160 * 1024)
         return set_err(NLOSGR_E_UNSUPPORTED, "occl / AABB engine: LDS budget");
     return NLOSGR_OK;
 }
@@ -883,7 +964,7 @@ int tiles_fwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosg
     if (rc) return rc;
     a.hist_out = hist_out;
     a.ray_out = ray_out;
-    const size_t shm = (size_t)TLayout(P.rt, geo->nr, tile_threads<false>()).total * sizeof(float);
+    const size_t shm = (size_t)TLayout(P.rt, geo->nr, tile_threads<false>(), false).total * sizeof(float);
     dispatch_tile<false>(a, shm, s);
     HIPCHK(hipGetLastError());
     if (hist_out) {
@@ -907,7 +988,7 @@ int tiles_bwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosg
     a.grad_ray = grad_ray;
     HIPCHK(hipMemsetAsync(a.acc, 0, (size_t)P.nslot * g->ng * kRec * sizeof(float), s));
     if (geo->nwall > 0 && (grad_hist || grad_ray)) {
-        const size_t shm = (size_t)TLayout(P.rt, geo->nr, tile_threads<true>()).total * sizeof(float);
+        const size_t shm = (size_t)TLayout(P.rt, geo->nr, tile_threads<true>(), true).total * sizeof(float);
         dispatch_tile<true>(a, shm, s);
         HIPCHK(hipGetLastError());
     }
