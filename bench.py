@@ -15,8 +15,9 @@ Default cutoff 5.7 sigma = the parity-grade support (pdf < 1e-7 of 
 rel-L2 vs the 6-sigma volume 1e-7).  `--lines 3.0` adds the same step at 3 sigma (the reference
 CUDA path's sigma_threshold; rel-L2 vs dense ~3e-2) under `lines` for comparison; never `value`.
 
-With N ranks (one process per GPU, RCCL): the relay wall is split into N contiguous bands, rank r
-renders band r and the packed gradients are summed with one all-reduce per step ->
+With N ranks (one process per GPU, RCCL): the relay wall is split into N shards of whole wall rows,
+row-interleaved (rank r renders rows r, r+N, ...: balanced work, nlosgr.distributed.wall_rows), and
+the packed gradients are summed with one bucketed all-reduce per step ->
 strong scaling, value = 1 volume per step / max-over-ranks step time.  --replicas instead gives
 every rank a full volume of its own capture (weak scaling).
 
@@ -230,7 +231,7 @@ def main():
         raise SystemExit("--band is a single-GPU projection; with N ranks the wall is sharded by default")
 
     from nlosgr import GaussianParams
-    from nlosgr.distributed import wall_band
+    from nlosgr.distributed import wall_rows
     from nlosgr.model import features_flat
     from nlosgr.render import count_support, render_forward
     from nlosgr.train import TrainStep
@@ -241,12 +242,13 @@ def main():
     model = GaussianParams.synthetic(ng, 3, preset=a.preset, device=dev, seed=0)
     sharded = world > 1 and not a.replicas
     walls_all = scene.walls(dev)
+    # shards: whole wall rows, row-interleaved over the ranks (balanced work; wall_rows)
     if sharded:
-        bands = [wall_band(H * W, rank, world)]
+        bands = [(rank, world)]
     elif a.band > 1:
-        bands = [wall_band(H * W, r, a.band) for r in range(a.band)]
+        bands = [(r, a.band) for r in range(a.band)]
     else:
-        bands = [(0, H * W)]
+        bands = [(0, 1)]
     g = torch.Generator().manual_seed(1 + (0 if sharded else rank))
     target_all = (torch.rand(H * W, T, generator=g) * 1e-3).to(dev)   # measured volume, x gt_times=100 in the loss
     stream = torch.cuda.current_stream(dev)
@@ -255,10 +257,11 @@ def main():
     for cut in cutoffs:
         cfg = make_config(model, scene, a.preset, a.mode, cutoff=cut, selection=a.selection)
         per_band = []
-        for (b0, b1) in bands:
-            whole = (b0, b1) == (0, H * W)
-            geo = scene.geometry(dev, a.preset, a.mode, walls=None if whole else walls_all[b0:b1].contiguous())
-            target = target_all[b0:b1].contiguous()
+        for (b0, b1) in bands:      # (shard, of shards)
+            whole = b1 == 1
+            idx = wall_rows(H, W, b0, b1, device=dev)
+            geo = scene.geometry(dev, a.preset, a.mode, walls=None if whole else walls_all[idx].contiguous())
+            target = target_all[idx].contiguous()
             ev_fwd = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
             ev_bwd = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
             train = TrainStep(model, geo, cfg, target, gt_times=100.0,
@@ -291,7 +294,7 @@ def main():
             per_band.append({"band": [b0, b1], "ms_per_step": elapsed * 1000.0 / a.steps,
                              "fwd_ms": statistics.fmean(fwd_ms), "bwd_ms": statistics.fmean(bwd_ms) if bwd_ms else 0.0,
                              "fwd_ms_all": fwd_ms, "bwd_ms_all": bwd_ms, "pairs": pairs, "rays": rays,
-                             "evaluations": evals, "nwall": b1 - b0})
+                             "evaluations": evals, "nwall": int(idx.numel())})
             del train, snap
             torch.cuda.empty_cache()
         results[cut] = per_band
@@ -346,9 +349,10 @@ def main():
                                f"{'fwd' if fwd_only else 'fwd+MSE+bwd (6 param grads)+Adam'}, frozen workload",
                    "gaussians": ng, "wall": [H, W], "bins": T, "angular": ns, "cutoff": a.cutoff,
                    "preset": a.preset, "mode": a.mode, "selection": a.selection,
-                   "parallelism": (f"wall shard: {world} bands (rank r renders band r), packed grad all-reduce"
+                   "parallelism": (f"wall shard: {world} row-interleaved shards (rank r renders wall rows r, r+{world}, ...), "
+                                   f"bucketed grad all-reduce"
                                    if sharded else
-                                   f"all {a.band} bands of a {a.band}-way wall shard timed in turn on one GPU "
+                                   f"all {a.band} shards of a {a.band}-way row-interleaved wall shard timed in turn on one GPU "
                                    f"(projected job rate = 1 / slowest band; all-reduce not timed)" if a.band > 1 else
                                    f"replicas x{world} (own capture each), grad all-reduce" if world > 1 else
                                    "single GPU")},

@@ -26,6 +26,18 @@ def wall_band(nwall, rank, world):
     return a, a + q + (1 if rank < r else 0)
 
 
+def wall_rows(H, W, rank, world, device=None):
+    """Row-interleaved shard of an H x W wall for `rank`: wall rows rank, rank + world, ... (row-major
+    wall-point indices, int64).  Every rank gets whole wall rows spread over the wall, so the
+    per-rank work is balanced (a contiguous band near the wall's centre sees more of the scene than
+    one at its edge: up to 1.07x the mean for C5's eight bands); counts differ by at most one row."""
+    if world < 1 or not 0 <= rank < world:
+        raise ValueError("nlosgr: bad rank/world")
+    rows = torch.arange(rank, H, world, dtype=torch.int64) if rank < H else torch.zeros(0, dtype=torch.int64)
+    idx = (rows.view(-1, 1) * W + torch.arange(W, dtype=torch.int64).view(1, -1)).reshape(-1)
+    return idx.to(device) if device is not None else idx
+
+
 def pack_grads(params):
     """Flatten the .grad of every parameter (zeros where missing) into one contiguous buffer."""
     flat = [(p.grad if p.grad is not None else torch.zeros_like(p)).reshape(-1) for p in params]

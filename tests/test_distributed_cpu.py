@@ -81,6 +81,24 @@ def test_wall_band_partition():
         wall_band(4, 2, 2)
 
 
+def test_wall_rows_partition():
+    """Row-interleaved shards (bench.py's N-rank split): every wall point exactly once, whole rows,
+    row counts within one of each other."""
+    from nlosgr.distributed import wall_rows
+    for H, W in ((1, 1), (7, 3), (128, 128), (256, 256)):
+        for world in (1, 2, 3, 8):
+            parts = [wall_rows(H, W, r, world) for r in range(world)]
+            allidx = torch.cat(parts).sort().values
+            assert torch.equal(allidx, torch.arange(H * W))
+            assert all(p.numel() % W == 0 for p in parts)
+            rows = [p.numel() // W for p in parts]
+            assert max(rows) - min(rows) <= 1
+            for r, p in enumerate(parts):
+                assert torch.equal(p.view(-1, W)[:, 0] // W, torch.arange(r, max(r, H), world))
+    with pytest.raises(ValueError):
+        wall_rows(4, 4, 2, 2)
+
+
 def test_pack_unpack_roundtrip():
     from nlosgr.distributed import pack_grads, unpack_grads
     ps = [torch.zeros(5, 3, requires_grad=True), torch.zeros(5, 1, 1, requires_grad=True)]
