@@ -276,7 +276,7 @@ struct Drain {
     float t;          // pos - ks (bin offset from the closest approach)
     float ga, al;     // log2 value(t) = ga t^2 + al   (noocl: al includes log2 w [+ log2 sin theta])
     float st;         // sin(theta_i) (kept separate only when per-ray outputs are written)
-    float sc, lwc, logT;  // netf: sigma c dT, log2(w c dT), log2 T at pos
+    float sc, wc, T;      // netf: sigma c dT, w c dT, transmittance T at pos (linear: one exp per bin)
     float beta, xlo, elo; // binint: dr sqrt(a/2), lower bin edge beta (kap - 1/2) and erfc(|xlo|)
     int rbase;        // RAYS: ray * nr
     int wrap;         // dense no-occlusion: bins [0, wrap) still to drain after the first piece [start, nr)
@@ -290,7 +290,7 @@ template <int MODE, bool DENSE>
 __device__ __forceinline__ constexpr bool dense_wrap() { return DENSE && MODE == NLOSGR_MODE_NOOCL; }
 
 template <int MODE, bool DENSE, bool RAYS>
-__device__ __forceinline__ bool drain_setup(const float* A, const float* u0, float lw, float sc, float lwc,
+__device__ __forceinline__ bool drain_setup(const float* A, const float* u0, float lw, float sc, float wc,
                                             float2 th, float2 ph, int i, int j, int np_, int nr, float mc2,
                                             float r0, float dr, float inv_dr, float f0log2, Drain& d, int stag = 0) {
     Ray R;
@@ -321,8 +321,8 @@ __device__ __forceinline__ bool drain_setup(const float* A, const float* u0, flo
     } else {
         d.al = -kHalfLog2e * R.m2min;
         d.sc = sc;
-        d.lwc = lwc;
-        d.logT = (float)R.kl * f0log2;
+        d.wc = wc;
+        d.T = fast_exp2((float)R.kl * f0log2);   // (1 + 1e-7)^kl: the empty bins before the segment
         d.st = th.x;
     }
     d.rbase = (i * np_ + j) * nr;
@@ -459,7 +459,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
 
     Drain d;
     d.pos = 0; d.rem = 0; d.t = 0.f; d.ga = 0.f; d.al = 0.f; d.st = 0.f;
-    d.sc = 0.f; d.lwc = 0.f; d.logT = 0.f; d.rbase = 0;
+    d.sc = 0.f; d.wc = 0.f; d.T = 0.f; d.rbase = 0;
     d.beta = 0.f; d.xlo = 0.f; d.elo = 0.f;
     d.wrap = 0; d.tw = 0.f;
     bool act = false;
@@ -468,7 +468,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
     for (int base = g_lo + wave * 64;; base += kBlock) {
         const bool have = base < g_hi;         // wave-uniform
         Pair P;
-        float lw = 0.f, sc = 0.f, lwc = 0.f;
+        float lw = 0.f, sc = 0.f, wc = 0.f;
         bool more = false;
         int ci = 0, cj = 0;
         unsigned long long crec0 = 0ull, crec1 = 0ull;   // CACHE: passing cells of this lane's box
@@ -487,7 +487,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
                 more = (P.w > 0.f) && P.i0 <= P.i1 && P.j0 <= P.j1;
                 lw = more ? flog2(P.w) : 0.f;
                 sc = P.sigma * cdt;
-                lwc = more ? flog2(P.w * cdt) : 0.f;
+                wc = more ? P.w * cdt : 0.f;
             }
             if (flags & 2) more = false;      // diagnostics: pair setup only
             npair += __builtin_popcountll(__builtin_amdgcn_ballot_w64(more));
@@ -516,12 +516,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
                 for (int c = 0; c < 3; ++c) u0[c] = __shfl(P.u0[c], slot);
                 const float lws = __shfl(lw, slot);
                 const float scs = MODE == NLOSGR_MODE_NETF ? __shfl(sc, slot) : 0.f;
-                const float lwcs = MODE == NLOSGR_MODE_NETF ? __shfl(lwc, slot) : 0.f;
+                const float wcs = MODE == NLOSGR_MODE_NETF ? __shfl(wc, slot) : 0.f;
                 bool got = false;
                 if (take && !(flags & 1)) {
                     // dense: consecutive queue entries start 37 bins apart (distinct claim keys)
                     const int stag = dense_wrap<MODE, DENSE>() ? (int)(((unsigned)(qhead + r) * 37u) % (unsigned)nr) : 0;
-                    got = drain_setup<MODE, DENSE, RAYS>(A, u0, lws, scs, lwcs, tth[i], tph[j], i, j, np_, nr, mc2,
+                    got = drain_setup<MODE, DENSE, RAYS>(A, u0, lws, scs, wcs, tth[i], tph[j], i, j, np_, nr, mc2,
                                                          r0, dr, inv_dr, f0log2, d, stag);
                     if (got) nsamp += (unsigned)(d.rem + (dense_wrap<MODE, DENSE>() ? d.wrap : 0));
                     act = got && !(flags & 4);    // diagnostics: segment records only
@@ -548,7 +548,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
             const int remw = win ? d.rem : 0;
             float* hb = hist + (win ? (QUAD ? (d.pos & ~(VW - 1)) : d.pos) : (QUAD ? padq : pad));
             float t = d.t;
-            float logT = d.logT;
+            float T = d.T;
             float xlo = d.xlo, elo = d.elo;
             if (QUAD) {
                 // kSteps bins from the even bin at or below pos: one ds_read_b64 + ds_write_b64 per 2
@@ -587,7 +587,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
                     }
                 }
                 t += (float)(kSteps - o);
-            } else
+            } else {
+            // netf, culled: pdf by the exp2 recurrence (kRecurrence), re-seeded per round
+            constexpr bool REC = MODE == NLOSGR_MODE_NETF && !DENSE;
+            float cur = 0.f, rq = 0.f, rcc = 0.f;
+            if (REC) {
+                cur = fast_exp2(fmaf(d.ga, t * t, d.al));
+                rq = fast_exp2(d.ga * fmaf(2.f, t, 1.f));
+                rcc = fast_exp2(2.f * d.ga);
+            }
 #pragma unroll
             for (int m = 0; m < kSteps; ++m) {
                 const bool in = m < remw;
@@ -614,11 +622,19 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
                         v *= d.st;
                     }
                 } else {
-                    const float pdf = fast_exp2(e2);
-                    const float lf = flog2(__expf(-d.sc * pdf) + 1e-7f);
-                    const float val = fast_exp2(d.lwc + logT) * pdf;
+                    // T_k = prod_{k' < k} (exp(-sigma pdf_k' c dT) + 1e-7), out_k = w c dT pdf_k T_k
+                    float pdf;
+                    if (REC) {
+                        pdf = cur;
+                        cur *= rq;
+                        rq *= rcc;
+                    } else {
+                        pdf = fast_exp2(e2);
+                    }
+                    const float f = __expf(-d.sc * pdf) + 1e-7f;
+                    const float val = d.wc * T * pdf;
                     if (RAYS && in) atomicAdd(rout + d.rbase + d.pos + m, rscale * val);
-                    logT += in ? lf : 0.f;
+                    T *= in ? f : 1.f;
                     v = in ? val * d.st : 0.f;
                 }
                 t += 1.f;
@@ -626,10 +642,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
                 hb[m] = x + v;
                 compiler_fence();
             }
+            }
             if (win) {
                 const int adv = QUAD ? kSteps - (d.pos & (VW - 1)) : kSteps;
                 d.t = t;
-                d.logT = logT;
+                d.T = T;
                 d.xlo = xlo;
                 d.elo = elo;
                 d.pos += adv;
@@ -1216,10 +1233,24 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
                     // dL/dD_j = c rho H_j T_j + (sum_{k>j} H_k out_k) f'_j / f_j  (two passes per ray)
                     float T = b.T, Etot = b.Etot, pre = b.pre;
                     float S0 = b.S0, S1 = b.S1, S2 = b.S2, dsig = b.dsig, drho = b.drho;
+                    // culled: pdf by the exp2 recurrence (kRecurrence), re-seeded per round
+                    float cur = 0.f, rq = 0.f, rcc = 0.f;
+                    if (!DENSE) {
+                        cur = fast_exp2(fmaf(b.c2, kap * kap, b.c0));
+                        rq = fast_exp2(b.c2 * fmaf(2.f, kap, 1.f));
+                        rcc = fast_exp2(2.f * b.c2);
+                    }
 #pragma unroll
                     for (int m = 0; m < kBSteps; ++m) {
                         const bool in = m < remw;
-                        const float pdf = fast_exp2(fmaf(b.c2, kap * kap, b.c0));
+                        float pdf;
+                        if (DENSE) {
+                            pdf = fast_exp2(fmaf(b.c2, kap * kap, b.c0));
+                        } else {
+                            pdf = cur;
+                            cur *= rq;
+                            rq *= rcc;
+                        }
                         const float D = b.sigma * pdf;
                         const float H = Hs[m];
                         const float ee = __expf(-D * cdt);
