@@ -888,8 +888,8 @@ struct BRay {
     float S0, S1, S2;
     float zs[3], v[3], ts, w;            // ray geometry for the closed-form result
     float rho, sigma;
-    float T, T0, Etot, pre, dsig, drho;  // netf
-    bool ph1;                            // netf: second pass
+    float T, pre, dsig, drho;            // netf: transmittance, prefix of H out, accumulators (part A)
+    float S0b, S1b, S2b, dsigb;          // netf: accumulators of part B (scaled by the ray's total at the end)
 };
 
 __device__ __forceinline__ void load_pdat(const float* pd, float* A, float* u0, float& w, float& rho, float& sigma) {
@@ -983,9 +983,9 @@ __device__ __forceinline__ bool bray_setup(const float* pd, float2 th, float2 ph
     b.ts = R.ts;
     b.w = w; b.rho = rho; b.sigma = sigma;
     if (MODE == NLOSGR_MODE_NETF) {
-        b.T = b.T0 = fast_exp2((float)R.kl * f0log2);
-        b.Etot = b.pre = b.dsig = b.drho = 0.f;
-        b.ph1 = false;
+        b.T = fast_exp2((float)R.kl * f0log2);
+        b.pre = b.dsig = b.drho = 0.f;
+        b.S0b = b.S1b = b.S2b = b.dsigb = 0.f;
     }
     return true;
 }
@@ -1125,8 +1125,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
         b.S0 = b.S1 = b.S2 = 0.f;
         b.zs[0] = b.zs[1] = b.zs[2] = b.v[0] = b.v[1] = b.v[2] = b.ts = b.w = 0.f;
         b.rho = b.sigma = 0.f;
-        b.T = b.T0 = b.Etot = b.pre = b.dsig = b.drho = 0.f;
-        b.ph1 = false;
+        b.T = b.pre = b.dsig = b.drho = 0.f;
+        b.S0b = b.S1b = b.S2b = b.dsigb = 0.f;
         // pending result of a finished ray: dL/du0, dL/dv, dsigma, drho
         float rU[3] = {0.f, 0.f, 0.f}, rV[3] = {0.f, 0.f, 0.f}, rSig = 0.f, rRho = 0.f;
         while (true) {
@@ -1230,9 +1230,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
                     }
                     b.S0 = S0; b.S1 = S1; b.S2 = S2;
                 } else {
-                    // dL/dD_j = c rho H_j T_j + (sum_{k>j} H_k out_k) f'_j / f_j  (two passes per ray)
-                    float T = b.T, Etot = b.Etot, pre = b.pre;
+                    // dL/dD_j = c rho H_j T_j + a_j (E - P_j),  a_j = f'_j / f_j = -c dT e_j / f_j, P_j = the
+                    // prefix sum of H_k out_k through bin j and E its total over the ray.  One pass: every
+                    // weighted sum sum_j dL/dD_j w_j splits into part A = sum_j (c rho H_j T_j - P_j a_j) w_j and
+                    // part B = sum_j a_j w_j, combined as A + E B once the ray is done (E = P at the end).
+                    float T = b.T, pre = b.pre;
                     float S0 = b.S0, S1 = b.S1, S2 = b.S2, dsig = b.dsig, drho = b.drho;
+                    float S0b = b.S0b, S1b = b.S1b, S2b = b.S2b, dsigb = b.dsigb;
                     // culled: pdf by the exp2 recurrence (kRecurrence), re-seeded per round
                     float cur = 0.f, rq = 0.f, rcc = 0.f;
                     if (!DENSE) {
@@ -1255,22 +1259,22 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
                         const float H = Hs[m];
                         const float ee = __expf(-D * cdt);
                         const float f = ee + 1e-7f;
-                        const float term = H * cdt * b.rho * D * T;
-                        if (!b.ph1) {
-                            Etot += term;
-                        } else {
-                            pre += term;
-                            const float dD = in ? cdt * b.rho * H * T + (Etot - pre) * (-cdt * ee) * frcp(f) : 0.f;
-                            drho += H * cdt * D * T;
-                            const float hp = dD * b.sigma * pdf;
-                            dsig += dD * pdf;
-                            const float t1 = hp * kap;
-                            S0 += hp; S1 += t1; S2 = fmaf(t1, kap, S2);
-                        }
+                        const float hdt = H * cdt * D * T;
+                        drho += hdt;
+                        pre = fmaf(b.rho, hdt, pre);
+                        const float a = in ? -cdt * ee * frcp(f) : 0.f;
+                        const float c1 = in ? fmaf(-pre, a, cdt * b.rho * H * T) : 0.f;
+                        const float hA = c1 * b.sigma * pdf, hB = a * b.sigma * pdf;
+                        dsig = fmaf(c1, pdf, dsig);
+                        dsigb = fmaf(a, pdf, dsigb);
+                        const float tA = hA * kap, tB = hB * kap;
+                        S0 += hA; S1 += tA; S2 = fmaf(tA, kap, S2);
+                        S0b += hB; S1b += tB; S2b = fmaf(tB, kap, S2b);
                         T *= in ? f : 1.f;
                         kap += 1.f;
                     }
-                    b.T = T; b.Etot = Etot; b.pre = pre;
+                    b.T = T; b.pre = pre;
+                    b.S0b = S0b; b.S1b = S1b; b.S2b = S2b; b.dsigb = dsigb;
                     b.S0 = S0; b.S1 = S1; b.S2 = S2; b.dsig = dsig; b.drho = drho;
                 }
                 if (act) {
@@ -1278,14 +1282,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
                         b.kap = kap;
                         b.pos += kBSteps - o;
                         b.rem -= kBSteps - o;
-                        if (MODE == NLOSGR_MODE_NETF && b.rem <= 0 && !b.ph1) {   // second pass from the start
-                            b.ph1 = true;
-                            b.pos = b.kl; b.rem = b.len; b.kap = b.kap0; b.T = b.T0;
-                        }
                     }
                     if (b.rem <= 0 && !pend) {
                         // pdf = exp(-|z|^2/2), z = z* + dl v:  dL/du0 = -sum P z,  dL/dv = -sum P dl z
-                        float S0 = b.S0, S1 = b.S1 * dr, S2 = b.S2 * dr * dr;
+                        float S0 = b.S0, S1 = b.S1, S2 = b.S2;
+                        if (MODE == NLOSGR_MODE_NETF) {   // A + E B, E = the ray's total (its final prefix)
+                            S0 = fmaf(b.pre, b.S0b, S0);
+                            S1 = fmaf(b.pre, b.S1b, S1);
+                            S2 = fmaf(b.pre, b.S2b, S2);
+                        }
+                        S1 *= dr;
+                        S2 *= dr * dr;
                         if (MODE == NLOSGR_MODE_NOOCL) {
                             if (!RAYS) { S0 *= b.st; S1 *= b.st; S2 *= b.st; }
                             // no-occlusion: dsigma = S0 rho, drho = S0 sigma; the pair lane applies its own
@@ -1294,7 +1301,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
                             rRho = 0.f;
                             S0 *= b.w; S1 *= b.w; S2 *= b.w;
                         } else {
-                            rSig = b.dsig;
+                            rSig = fmaf(b.pre, b.dsigb, b.dsig);
                             rRho = b.drho;
                         }
                         for (int r = 0; r < 3; ++r) {
