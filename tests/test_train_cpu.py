@@ -24,3 +24,17 @@ def test_optimization_defaults_match_reference_config():
         (0.00016, 0.0000016, 0.01, 50_000)
     assert (o.feature_lr, o.opacity_lr, o.scaling_lr, o.rotation_lr) == (0.0025, 0.025, 0.005, 0.001)
     assert (o.regularization, o.scale_reg, o.opacity_reg) == (False, 0.01, 0.01)
+
+
+def test_rendering_type_dispatch():
+    """nlos_helpers dispatch (nlos_helpers.py:200-212, gaussian_model.py:297-364): occlusion off ->
+    no-occlusion sum; 'netf' -> per-Gaussian self-transmittance; 'nlos-neus' crashes in the reference
+    (gaussian_model.py:336 shape mismatch) and is rejected explicitly here."""
+    from types import SimpleNamespace
+    import pytest
+    from nlosgr.nlos_helpers import _mode
+    assert _mode(SimpleNamespace(occlusion=False, rendering_type="nlos-neus")) == "noocl"
+    assert _mode(SimpleNamespace(occlusion=True, rendering_type="netf")) == "netf"
+    assert _mode(SimpleNamespace(occlusion=True)) == "netf"
+    with pytest.raises(NotImplementedError):
+        _mode(SimpleNamespace(occlusion=True, rendering_type="nlos-neus"))
