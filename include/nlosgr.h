@@ -117,7 +117,11 @@ typedef struct {
                                  of its candidate box are in support (20 B per pair in the workspace,
                                  see nlosgr_workspace_bytes) and a backward on the SAME workspace with
                                  the SAME inputs walks that record instead of re-testing the rays.
-                                 Culled (cutoff > 0), histogram-only calls; 0 = off */
+                                 Culled (cutoff > 0), histogram-only calls.  In NLOSGR_MODE_OCCL it is
+                                 the row cache instead: the forward stores every ray tile's (D, W) rows
+                                 (8 B per wall point x ray x bin; C3 128 GiB) and the backward on the
+                                 same workspace reloads them instead of re-running its forward sweep.
+                                 0 = off */
     int32_t selection;        /* NLOSGR_SELECT_*.  OCCL mode and AABB selection run the ray-tile engine
                                  (ray-major, per-ray compositing, deterministic); the ray cache and
                                  nlosgr_count_support do not apply there */
@@ -127,7 +131,8 @@ typedef struct {
 } nlosgr_options;
 
 /* Scratch bytes needed by fwd/bwd for this problem (caller allocates, 256-B aligned); includes
- * nwall*ng*20 B for the ray cache when opt->ray_cache is set. */
+ * nwall*ng*24 B for the ray cache when opt->ray_cache is set (OCCL mode: the row cache,
+ * nwall * tiles * tile rays * nr * 8 B). */
 NLOSGR_API size_t nlosgr_workspace_bytes(const nlosgr_gaussians* g, const nlosgr_geometry* geo,
                               const nlosgr_options* opt);
 

@@ -195,7 +195,7 @@ __device__ void chain_to_raw(const nlosgr_gaussians& g, int i, const float* acc,
 // ray-tile engine (nlosgr_tiles.hip): NLOSGR_MODE_OCCL and NLOSGR_SELECT_AABB
 bool tiles_engine(const nlosgr_options* opt);
 int tiles_validate(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_options* opt);
-size_t tiles_workspace_bytes(const nlosgr_gaussians* g, const nlosgr_geometry* geo);
+size_t tiles_workspace_bytes(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_options* opt);
 int tiles_fwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_options* opt, void* ws,
               float* hist_out, float* ray_out, hipStream_t s);
 int tiles_bwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_options* opt, void* ws,

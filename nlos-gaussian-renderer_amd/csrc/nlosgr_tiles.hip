@@ -82,6 +82,8 @@ struct TArgs {
     long long nitems;
     int nslot;
     unsigned long long* diag;   // NLOSGR_TILES_DIAG: per-phase cycles of thread 0, summed over workgroups
+    float2* rcache;          // OCCL row cache [nitems][rt][nr] (D, W) (opt.ray_cache): the forward's rows,
+                             // reloaded by the backward instead of re-running its first sweep
 };
 
 __host__ __device__ inline int tile_rays(int nr) {
@@ -275,8 +277,16 @@ __global__ __launch_bounds__(tile_threads<BWD>()) void tile_kernel(TArgs k) {
                 if (tid < 64) icnt[tid] = 0;
                 __syncthreads();
             }
+            // backward, first sweep: without occlusion the scan needs no (D, W) rows at all; with the
+            // row cache they are the forward's, reloaded (coalesced) instead of recomputed
+            const bool skip0 = BWD && !pairs && (!OCCL || k.rcache != nullptr);
+            if (BWD && !pairs && OCCL && k.rcache) {
+                const float2* src = k.rcache + (size_t)item * RT * nr;
+                for (int x = tid; x < RT * nr; x += kTB) rows[x] = src[x];
+                __syncthreads();
+            }
             int qn = 0;
-            for (int g0 = 0; g0 < k.g.ng || qn > 0; g0 += kTB) {
+            for (int g0 = 0; !skip0 && (g0 < k.g.ng || qn > 0); g0 += kTB) {
                 // ---- cull round: lane = Gaussian, 512 per round, ordered append ----
                 if (g0 < k.g.ng) {
                     const int gi = g0 + tid;
@@ -709,6 +719,11 @@ __global__ __launch_bounds__(tile_threads<BWD>()) void tile_kernel(TArgs k) {
 
             if (!pairs) {
                 TDIAG(trays)
+                if (!BWD && OCCL && k.rcache) {   // record the (D, W) rows for the backward
+                    float2* dst = k.rcache + (size_t)item * RT * nr;
+                    for (int x = tid; x < RT * nr; x += kTB) dst[x] = rows[x];
+                    __syncthreads();
+                }
                 // ---------------- scan: wave = ray, lane = bin ----------------
                 for (int r = wave; r < RT; r += kTW) {
                     const int i = ti0 + r / k.tj, j = tj0 + r % k.tj;
@@ -832,10 +847,13 @@ int cu_count() {
 struct TPlan {
     int rt, ti, tj, nti, ntj, ntiles, nslot;
     long long nitems;
-    size_t off_cull, off_bbox, off_acc, off_hpart, total;
+    size_t off_cull, off_bbox, off_acc, off_hpart, off_rows, total;
 };
 
-TPlan plan(const nlosgr_gaussians* g, const nlosgr_geometry* geo) {
+// the OCCL row cache: 8 B per (item, tile ray, bin), e.g. C3 (128x128 wall, 32x32 rays, 1024 bins) 128 GiB
+bool row_cache(const nlosgr_options* opt) { return opt && opt->ray_cache && opt->mode == NLOSGR_MODE_OCCL; }
+
+TPlan plan(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_options* opt) {
     TPlan P;
     P.rt = tile_rays(geo->nr);
     int ti = 1;
@@ -853,7 +871,8 @@ TPlan plan(const nlosgr_gaussians* g, const nlosgr_geometry* geo) {
     P.off_bbox = P.off_cull + align_up(ng * sizeof(float4));
     P.off_acc = P.off_bbox + align_up(ng * 6 * sizeof(float));
     P.off_hpart = P.off_acc + align_up((size_t)P.nslot * ng * kRec * sizeof(float));
-    P.total = P.off_hpart + align_up((size_t)geo->nwall * P.ntiles * geo->nr * sizeof(float));
+    P.off_rows = P.off_hpart + align_up((size_t)geo->nwall * P.ntiles * geo->nr * sizeof(float));
+    P.total = P.off_rows + (row_cache(opt) ? align_up((size_t)P.nitems * P.rt * geo->nr * sizeof(float2)) : 0);
     return P;
 }
 
@@ -913,6 +932,7 @@ int prepare(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_
     a.ti = P.ti; a.tj = P.tj; a.rt = P.rt;
     a.ntile_i = P.nti; a.ntile_j = P.ntj; a.ntiles = P.ntiles;
     a.nitems = P.nitems; a.nslot = P.nslot;
+    a.rcache = row_cache(opt) ? (float2*)(base + P.off_rows) : nullptr;
     launch_preprocess(g, (GaussRec*)base, s);
     HIPCHK(hipGetLastError());
     const int nb = (g->ng + 255) / 256;
@@ -948,12 +968,14 @@ int tiles_validate(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const 
     return NLOSGR_OK;
 }
 
-size_t tiles_workspace_bytes(const nlosgr_gaussians* g, const nlosgr_geometry* geo) { return plan(g, geo).total; }
+size_t tiles_workspace_bytes(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_options* opt) {
+    return plan(g, geo, opt).total;
+}
 
 int tiles_fwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_options* opt, void* ws,
               float* hist_out, float* ray_out, hipStream_t s) {
     if (!ws) return set_err(NLOSGR_E_INVALID, "workspace is null");
-    const TPlan P = plan(g, geo);
+    const TPlan P = plan(g, geo, opt);
     if (ray_out) HIPCHK(hipMemsetAsync(ray_out, 0, (size_t)geo->nwall * geo->nt * geo->np * geo->nr * sizeof(float), s));
     if (g->ng == 0) {
         if (hist_out) HIPCHK(hipMemsetAsync(hist_out, 0, (size_t)geo->nwall * geo->nr * sizeof(float), s));
@@ -980,7 +1002,7 @@ int tiles_bwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosg
               const float* grad_hist, const float* grad_ray, float* d_mu, float* d_scaling, float* d_rotation,
               float* d_opacity, float* d_features, hipStream_t s) {
     if (!ws) return set_err(NLOSGR_E_INVALID, "workspace is null");
-    const TPlan P = plan(g, geo);
+    const TPlan P = plan(g, geo, opt);
     TArgs a;
     int rc = prepare(g, geo, opt, ws, P, a, s);
     if (rc) return rc;

@@ -1723,7 +1723,7 @@ const char* nlosgr_last_error(void) { return g_err; }
 
 size_t nlosgr_workspace_bytes(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_options* opt) {
     if (validate(g, geo, opt) != NLOSGR_OK) return 0;
-    if (tiles_engine(opt)) return tiles_workspace_bytes(g, geo);
+    if (tiles_engine(opt)) return tiles_workspace_bytes(g, geo, opt);
     const size_t rec = align_up((size_t)g->ng * sizeof(GaussRec));
     const size_t part = align_up((size_t)bwd_nsplit_ws(g, geo, opt) * g->ng * 32 * sizeof(float));
     return rec + part + cache_bytes(g, geo, opt) + sh_bytes(g, geo) + 256 + fpart_bytes(g, geo);

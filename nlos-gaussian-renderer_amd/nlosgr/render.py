@@ -39,8 +39,27 @@ class RenderConfig:
                                  # first 256 Gaussians per ray by index; cuda preset)
 
 
+def tile_rows_bytes(geo):
+    """Bytes of the occlusion engine's row cache: one (D, W) float2 per (wall point, ray, bin), rays
+    padded to whole tiles (tile_rays / plan in csrc/nlosgr_tiles.hip); C3: 128 GiB."""
+    nr = geo.nr
+    rt = 64
+    while rt > 4 and 2 * rt * nr > 32768:
+        rt >>= 1
+    ti = 1
+    while ti * ti < rt:
+        ti <<= 1
+    tj = rt // ti
+    ntiles = (-(-geo.nt // ti)) * (-(-geo.np // tj))
+    return geo.nwall * ntiles * rt * nr * 8
+
+
 def use_ray_cache(cfg, geo, ng, want_rays=False):
-    """The forward->backward ray cache applies to culled, histogram-only, differentiable modes."""
+    """The forward->backward cache: for the culled, histogram-only pair-major modes the in-support rays
+    of every pair; for occlusion compositing the tiles' (D, W) rows, which spares the backward its
+    re-run of the forward sweep."""
+    if cfg.mode == "occl":
+        return bool(cfg.ray_cache) and not want_rays and tile_rows_bytes(geo) <= RAY_CACHE_MAX_BYTES
     return (bool(cfg.ray_cache) and 0 < cfg.cutoff <= RAY_CACHE_MAX_CUTOFF and not want_rays
             and cfg.mode in ("noocl", "netf") and cfg.selection == "support"
             and geo.nwall * ng * 24 <= RAY_CACHE_MAX_BYTES)

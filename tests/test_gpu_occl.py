@@ -182,3 +182,28 @@ def test_train_step_occl():
     for _ in range(5):
         l1 = float(step()[0])
     assert np.isfinite(l1) and l1 < l0
+
+
+@pytest.mark.parametrize("selection,cutoff", [("support", 5.7), ("support", 0.0), ("aabb", 0.0)])
+def test_occl_row_cache_backward_equals_recompute(selection, cutoff):
+    """The occlusion row cache (ray_cache=True: the forward stores every tile's (D, W) rows in the
+    workspace and the backward reloads them instead of re-running its forward sweep) changes nothing:
+    gradients bitwise equal to the recomputing backward, forward unchanged."""
+    from nlosgr import features_flat
+    from nlosgr.geometry import build_geometry
+    from nlosgr.render import RenderConfig, render_backward, render_forward
+    walls, box = _scene()
+    m = _model(90, 3, 23, 1.0, 1.0)
+    geo = build_geometry(walls, box, NS, START, START + T, C, DELTAT, 0.5, "cuda", "occl")
+    cfg = RenderConfig(preset="cuda", mode="occl", sh_degree=3, cutoff=cutoff, c_deltaT=C * DELTAT,
+                       selection=selection)
+    args = (m._mu, m._scaling, m._rotation, m._opacity, features_flat(m).detach())
+    h0, _ = render_forward(*args, geo, cfg)
+    h1, _, ws = render_forward(*args, geo, cfg, ray_cache=True)
+    assert torch.equal(h0, h1)
+    gh = torch.randn_like(h0)
+    d0 = render_backward(*args, geo, cfg, grad_hist=gh)
+    d1 = render_backward(*args, geo, cfg, grad_hist=gh, workspace=ws, ray_cache=True)
+    assert any(bool(x.abs().max() > 0) for x in d0)
+    for a, b in zip(d0, d1):
+        assert torch.equal(a, b)
