@@ -651,8 +651,17 @@ __global__ __launch_bounds__(tile_threads<BWD>()) void tile_kernel(TArgs k) {
                             for (int x = 0; x < 14; ++x) any |= cb[x] != 0.f;
                             if (any) {
                                 const int gi = queue[e];
-                                const GaussRec rec = k.recs[gi];
-                                const float q[3] = {px - rec.a.x, py - rec.a.y, pz - rec.a.z};
+                                // the slot row, the Gaussian's mean and its SH row are loaded up front so the
+                                // three memory round trips overlap (the row was read after the compute)
+                                float4* dst = reinterpret_cast<float4*>(k.acc + ((size_t)blockIdx.x * k.g.ng + gi) * kRec);
+                                float4 acc4[kRec / 4];
+#pragma unroll
+                                for (int x = 0; x < kRec / 4; ++x) acc4[x] = dst[x];
+                                const float4 mu4 = k.recs[gi].a;
+                                float fr[kMaxK];
+#pragma unroll
+                                for (int c = 0; c < kMaxK; ++c) fr[c] = c < K ? k.g.features[(size_t)gi * k.g.k_feat + c] : 0.f;
+                                const float q[3] = {px - mu4.x, py - mu4.y, pz - mu4.z};
                                 float rec32[kRec];
                                 for (int x = 0; x < kRec; ++x) rec32[x] = 0.f;
                                 // dA += (sum gU0) q^T; dmu = -A^T sum gU0 (+ the view-direction chain)
@@ -666,7 +675,7 @@ __global__ __launch_bounds__(tile_threads<BWD>()) void tile_kernel(TArgs k) {
                                 view_dir<NLOSGR_PRESET_CUDA>(-q[0], -q[1], -q[2], dx, dy, dz, nrm);
                                 float Y[kMaxK];
                                 sh_basis<NLOSGR_PRESET_CUDA>(deg, dx, dy, dz, Y);
-                                const float* f = k.g.features + (size_t)gi * k.g.k_feat;
+                                const float* f = fr;
                                 const float sh = sh_dot(f, Y, K);
                                 const float gr = sh + 0.5f >= 0.f ? cb[13] : 0.f;
                                 if (gr != 0.f) {
@@ -679,9 +688,9 @@ __global__ __launch_bounds__(tile_threads<BWD>()) void tile_kernel(TArgs k) {
                                                                      ox, oy, oz);
                                     rec32[9] += ox; rec32[10] += oy; rec32[11] += oz;
                                 }
-                                float4* dst = reinterpret_cast<float4*>(k.acc + ((size_t)blockIdx.x * k.g.ng + gi) * kRec);
+#pragma unroll
                                 for (int x = 0; x < kRec / 4; ++x) {
-                                    float4 v = dst[x];
+                                    float4 v = acc4[x];
                                     v.x += rec32[4 * x]; v.y += rec32[4 * x + 1]; v.z += rec32[4 * x + 2]; v.w += rec32[4 * x + 3];
                                     dst[x] = v;
                                 }
