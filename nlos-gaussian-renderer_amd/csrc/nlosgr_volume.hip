@@ -1291,8 +1291,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
                             S1 = fmaf(b.pre, b.S1b, S1);
                             S2 = fmaf(b.pre, b.S2b, S2);
                         }
-                        S1 *= dr;
-                        S2 *= dr * dr;
+                        S1 = S1 * dr;
+                        S2 = S2 * dr * dr;
                         if (MODE == NLOSGR_MODE_NOOCL) {
                             if (!RAYS) { S0 *= b.st; S1 *= b.st; S2 *= b.st; }
                             // no-occlusion: dsigma = S0 rho, drho = S0 sigma; the pair lane applies its own
