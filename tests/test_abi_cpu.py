@@ -104,3 +104,24 @@ def test_dropin_renderers_fail_loudly_without_gpu():
         cuda_renderer.create_renderer(3.0)
     with pytest.raises(RuntimeError):
         cuda_renderer.NLOSGaussianRenderer()
+
+
+@pytest.mark.parametrize("nwall,nt,np_,nr", [(6, 32, 32, 1024), (3, 7, 5, 40), (2, 32, 32, 2048), (1, 9, 13, 77)])
+def test_occl_row_cache_size_matches_library(nwall, nt, np_, nr):
+    """render.tile_rows_bytes (the size the Python side checks before enabling the occlusion row
+    cache) equals the extra workspace the library plans for it (nlosgr_workspace_bytes with
+    ray_cache on minus off; host-only call, no GPU)."""
+    from types import SimpleNamespace
+    from nlosgr import _lib
+    from nlosgr.render import tile_rows_bytes
+    lib = _lib.load()
+    fake = ctypes.c_void_p(4096)   # validation only checks that the pointers are set
+    g = _lib.Gaussians(1000, 16, 3, _lib.PRESET_CUDA, 1.0, fake, fake, fake, fake, fake)
+    geo = _lib.Geometry(nwall, nt, np_, nr, *([fake] * 9))
+    sizes = []
+    for cache in (0, 1):
+        opt = _lib.Options(_lib.MODE_OCCL, 3.0, 0.01, 1.0, 0, 0, cache, _lib.SELECT_SUPPORT, 0, 0)
+        sizes.append(lib.nlosgr_workspace_bytes(g, geo, opt))
+    assert sizes[0] > 0, lib.nlosgr_last_error()
+    want = tile_rows_bytes(SimpleNamespace(nwall=nwall, nt=nt, np=np_, nr=nr))
+    assert sizes[1] - sizes[0] == (want + 255) // 256 * 256
