@@ -221,6 +221,7 @@ __global__ __launch_bounds__(tile_threads<BWD>()) void tile_kernel(TArgs k) {
     const float dr = nr > 1 ? (k.geo.r[nr - 1] - r0) / (float)(nr - 1) : 1.0f;
     const float inv_dr = 1.0f / dr;
     const float cdt = k.opt.c_deltaT;
+    const float ncdt = -cdt * kLog2e;   // exp(-x c dT) = exp2(x ncdt)
     const int nch = (nr + 63) / 64;
     const int deg = k.g.sh_degree, K = (deg + 1) * (deg + 1);
 
@@ -418,7 +419,7 @@ __global__ __launch_bounds__(tile_threads<BWD>()) void tile_kernel(TArgs k) {
                                     if (inp) {
                                         el[2 * (lrank - pb)] = make_float4(ks, ga, al, sg);
                                         el[2 * (lrank - pb) + 1] =
-                                            make_float4(rho, __int_as_float(kl), __int_as_float(kh), 0.f);
+                                            make_float4(rho, __int_as_float(kl), __int_as_float(kh - kl), 0.f);
                                     }
                                     wave_sync();
                                     const int lo = wave_min_i(inp ? kl : nr);
@@ -436,13 +437,14 @@ __global__ __launch_bounds__(tile_threads<BWD>()) void tile_kernel(TArgs k) {
                                             cm &= cm - 1;
                                             const int idx = __popcll(pm & ((1ull << s) - 1ull));
                                             const float4 e0 = el[2 * idx], e1 = el[2 * idx + 1];
-                                            const int skl = __float_as_int(e1.y), skh = __float_as_int(e1.z);
+                                            const int skl = __float_as_int(e1.y), slen = __float_as_int(e1.z);   // kh - kl
                                             const float tt = kf - e0.x;
                                             const float pdf = fast_exp2(fmaf(e0.y, tt * tt, e0.z));
-                                            const float cv = (kb >= skl && kb <= skh) ? e0.w * pdf : 0.f;
+                                            // kl <= kb <= kh as one unsigned range compare
+                                            const float cv = (unsigned)(kb - skl) <= (unsigned)slen ? e0.w * pdf : 0.f;
                                             if (OCCL) {
                                                 accD += cv;
-                                                accW = fmaf(e1.x, 1.0f - fast_exp2(-cv * cdt * kLog2e), accW);
+                                                accW = fmaf(e1.x, 1.0f - fast_exp2(cv * ncdt), accW);
                                             } else {
                                                 accW = fmaf(e1.x, cv, accW);
                                             }
