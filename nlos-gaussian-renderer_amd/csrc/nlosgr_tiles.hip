@@ -579,15 +579,16 @@ __global__ __launch_bounds__(tile_threads<BWD>()) void tile_kernel(TArgs k) {
                                 const float al = -0.5f * kLog2e * m2min;
                                 float m0 = 0.f, m1 = 0.f, m2 = 0.f, ps = 0.f, pr = 0.f;
                                 const float2* row = rows + (rg + 4 * (4 * rb + kk)) * nr;
-                                for (int kb = kl; kb <= kh; ++kb) {
-                                    const float tt = (float)kb - ks;
+                                const float rc = wrho * cdt;
+                                float tt = (float)kl - ks;   // bin offset from the closest approach, stepped by 1
+                                for (int kb = kl; kb <= kh; ++kb, tt += 1.f) {
                                     const float pdf = fast_exp2(fmaf(ga, tt * tt, al));
                                     const float cv = wsg * pdf;
                                     const float2 ab = row[kb];
                                     float dc;
                                     if (OCCL) {
-                                        const float ex = fast_exp2(-cv * cdt * kLog2e);
-                                        dc = fmaf(ab.x * wrho * cdt, ex, ab.y);
+                                        const float ex = fast_exp2(cv * ncdt);
+                                        dc = fmaf(ab.x * rc, ex, ab.y);
                                         pr = fmaf(ab.x, 1.0f - ex, pr);
                                     } else {
                                         dc = ab.x * wrho;
