@@ -590,6 +590,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
             } else {
             // netf, culled: pdf by the exp2 recurrence (kRecurrence), re-seeded per round
             constexpr bool REC = MODE == NLOSGR_MODE_NETF && !DENSE;
+            const float nsc = -d.sc * (2.f * kHalfLog2e);   // exp(-sigma c dT pdf) = exp2(pdf nsc)
             float cur = 0.f, rq = 0.f, rcc = 0.f;
             if (REC) {
                 cur = fast_exp2(fmaf(d.ga, t * t, d.al));
@@ -631,7 +632,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
                     } else {
                         pdf = fast_exp2(e2);
                     }
-                    const float f = __expf(-d.sc * pdf) + 1e-7f;
+                    const float f = fast_exp2(pdf * nsc) + 1e-7f;
                     const float val = d.wc * T * pdf;
                     if (RAYS && in) atomicAdd(rout + d.rbase + d.pos + m, rscale * val);
                     T *= in ? f : 1.f;
@@ -1237,6 +1238,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
                     float T = b.T, pre = b.pre;
                     float S0 = b.S0, S1 = b.S1, S2 = b.S2, dsig = b.dsig, drho = b.drho;
                     float S0b = b.S0b, S1b = b.S1b, S2b = b.S2b, dsigb = b.dsigb;
+                    const float kE = -cdt * (2.f * kHalfLog2e) * b.sigma, ncdt = -cdt, crho = cdt * b.rho;
                     // culled: pdf by the exp2 recurrence (kRecurrence), re-seeded per round
                     float cur = 0.f, rq = 0.f, rcc = 0.f;
                     if (!DENSE) {
@@ -1255,16 +1257,18 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
                             cur *= rq;
                             rq *= rcc;
                         }
-                        const float D = b.sigma * pdf;
+                        // per-ray constants folded: sp = sigma pdf, exp(-sp c dT) = exp2(pdf kE)
+                        const float sp = b.sigma * pdf;
                         const float H = Hs[m];
-                        const float ee = __expf(-D * cdt);
+                        const float ee = fast_exp2(pdf * kE);
                         const float f = ee + 1e-7f;
-                        const float hdt = H * cdt * D * T;
+                        const float HT = H * T;
+                        const float hdt = HT * (cdt * sp);
                         drho += hdt;
                         pre = fmaf(b.rho, hdt, pre);
-                        const float a = in ? -cdt * ee * frcp(f) : 0.f;
-                        const float c1 = in ? fmaf(-pre, a, cdt * b.rho * H * T) : 0.f;
-                        const float hA = c1 * b.sigma * pdf, hB = a * b.sigma * pdf;
+                        const float a = in ? (ee * ncdt) * frcp(f) : 0.f;
+                        const float c1 = in ? fmaf(-pre, a, crho * HT) : 0.f;
+                        const float hA = c1 * sp, hB = a * sp;
                         dsig = fmaf(c1, pdf, dsig);
                         dsigb = fmaf(a, pdf, dsigb);
                         const float tA = hA * kap, tB = hB * kap;
