@@ -323,6 +323,10 @@ __global__ __launch_bounds__(tile_threads<BWD>()) void tile_kernel(TArgs k) {
                     if (tid < nst) {
                         const int gi = queue[tid];
                         const GaussRec rec = k.recs[gi];
+                        // the SH row is loaded with the record (its round trip overlaps the record's)
+                        float fr[kMaxK];
+#pragma unroll
+                        for (int c = 0; c < kMaxK; ++c) fr[c] = c < K ? k.g.features[(size_t)gi * k.g.k_feat + c] : 0.f;
                         float* o = stage + tid * kStage;
                         const float A[9] = {rec.b.x, rec.b.y, rec.b.z, rec.b.w, rec.c.x, rec.c.y, rec.c.z, rec.c.w, rec.d.x};
                         const float q0 = px - rec.a.x, q1 = py - rec.a.y, q2 = pz - rec.a.z;
@@ -351,7 +355,7 @@ __global__ __launch_bounds__(tile_threads<BWD>()) void tile_kernel(TArgs k) {
                         view_dir<NLOSGR_PRESET_CUDA>(-q0, -q1, -q2, dx, dy, dz, nrm);
                         float Y[kMaxK];
                         sh_basis<NLOSGR_PRESET_CUDA>(deg, dx, dy, dz, Y);
-                        const float sh = sh_dot(k.g.features + (size_t)gi * k.g.k_feat, Y, K);
+                        const float sh = sh_dot(fr, Y, K);
                         o[19] = fmaxf(sh + 0.5f, 0.0f);
                     }
                     __syncthreads();
