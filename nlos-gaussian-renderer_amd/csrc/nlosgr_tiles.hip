@@ -585,10 +585,15 @@ __global__ __launch_bounds__(tile_threads<BWD>()) void tile_kernel(TArgs k) {
                                 const float2* row = rows + (rg + 4 * (4 * rb + kk)) * nr;
                                 const float rc = wrho * cdt;
                                 float tt = (float)kl - ks;   // bin offset from the closest approach, stepped by 1
+                                // the rows are read-only here: reads run two bins ahead of their use (past the
+                                // segment end they stay inside the LDS allocation and are not used)
+                                float2 ab0 = row[kl], ab1 = row[kl + 1];
                                 for (int kb = kl; kb <= kh; ++kb, tt += 1.f) {
                                     const float pdf = fast_exp2(fmaf(ga, tt * tt, al));
                                     const float cv = wsg * pdf;
-                                    const float2 ab = row[kb];
+                                    const float2 ab = ab0;
+                                    ab0 = ab1;
+                                    ab1 = row[kb + 2];
                                     float dc;
                                     if (OCCL) {
                                         const float ex = fast_exp2(cv * ncdt);
