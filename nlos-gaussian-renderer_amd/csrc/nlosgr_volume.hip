@@ -321,7 +321,7 @@ __device__ __forceinline__ bool drain_setup(const float* A, const float* u0, flo
     } else {
         d.al = -kHalfLog2e * R.m2min;
         d.sc = sc;
-        d.wc = wc;
+        d.wc = RAYS ? wc : wc * th.x;   // histogram-only: sin(theta) folded into the weight
         d.T = fast_exp2((float)R.kl * f0log2);   // (1 + 1e-7)^kl: the empty bins before the segment
         d.st = th.x;
     }
@@ -636,7 +636,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
                     const float val = d.wc * T * pdf;
                     if (RAYS && in) atomicAdd(rout + d.rbase + d.pos + m, rscale * val);
                     T *= in ? f : 1.f;
-                    v = in ? val * d.st : 0.f;
+                    v = in ? (RAYS ? val * d.st : val) : 0.f;
                 }
                 t += 1.f;
                 const float x = hb[m];
