@@ -254,8 +254,14 @@ __device__ __forceinline__ unsigned pack_ray(int slot, int i, int j) {
 // next round).  Lanes that did not win, or ran past their segment, point at private pad bins
 // and add 0, so the step body is branch-free.  Idle lanes are refilled from the ray queue.
 constexpr int kSteps = 24;     // bins per lane per drain round
-constexpr int kRefill = 32;    // refill once this many lanes are idle (or the queue is final)
-constexpr int kBRefill = 8;  // backward: same rule
+#ifndef NLOSGR_REFILL
+#define NLOSGR_REFILL 48
+#endif
+#ifndef NLOSGR_BREFILL
+#define NLOSGR_BREFILL 16
+#endif
+constexpr int kRefill = NLOSGR_REFILL;     // refill once this many lanes are idle (or the queue is final)
+constexpr int kBRefill = NLOSGR_BREFILL;   // backward: same rule
 
 struct FwdLayout {
     int hist, owner, rayq, wave_stride, total;  // offsets in floats
