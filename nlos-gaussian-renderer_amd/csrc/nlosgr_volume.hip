@@ -253,7 +253,10 @@ __device__ __forceinline__ unsigned pack_ray(int slot, int i, int j) {
 // start bins differ — guaranteed per round by a claim table (owner[pos] = lane; losers retry
 // next round).  Lanes that did not win, or ran past their segment, point at private pad bins
 // and add 0, so the step body is branch-free.  Idle lanes are refilled from the ray queue.
-constexpr int kSteps = 24;     // bins per lane per drain round
+#ifndef NLOSGR_FSTEPS
+#define NLOSGR_FSTEPS 20
+#endif
+constexpr int kSteps = NLOSGR_FSTEPS;     // bins per lane per drain round
 #ifndef NLOSGR_REFILL
 #define NLOSGR_REFILL 48
 #endif
@@ -846,7 +849,10 @@ __global__ __launch_bounds__(kBlock) void fwd_dense_kernel(KArgs k) {
 // its pair: finished lanes claim owner[slot] with a round stamp, each pair lane gathers its
 // claimant's result with ds_bpermute and folds it into the Gaussian's register accumulators.
 // Losers keep their result and retry next round.  No LDS float atomics, no pair/row tables.
-constexpr int kBSteps = 24;   // bins per lane per backward drain round
+#ifndef NLOSGR_BSTEPS
+#define NLOSGR_BSTEPS 24
+#endif
+constexpr int kBSteps = NLOSGR_BSTEPS;   // bins per lane per backward drain round
 constexpr int kBwdSlots = 13;   // per-Gaussian backward partial: dA[9], dMu[3], dsigma (stride 32 in HBM)
 constexpr int kShPart = 28;     // sh_kernel partial: dF[KM <= 25], dMu[3] (at KM), pad
 
