@@ -325,7 +325,8 @@ def main():
     traffic, traffic_src = pmc_traffic(a.config, kern, a.cutoff) if single else (None, None)
     # compute-side figures: exact in-support evaluations of the (frozen) workload per second, and the
     # VALU issue utilisation from the committed SQ counter pass of this command
-    # (SQ_INSTS_VALU x 2 cycles per wave64 instruction / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs))
+    # (SQ_INSTS_VALU x 2 cycles per wave64 instruction / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs); the 2
+    # cycles: MI355X_MICROARCH.md:54,473; v_exp_f32 measured at 8.2 (scripts/drain_proto.hip), so a lower bound)
     ev = worst["evaluations"]
     valu = {"evaluations": ev, "pairs": worst["pairs"], "rays": worst["rays"],
             "evals_per_s_fwd": ev / (fwd_avg * 1e-3) if ev else None,

@@ -21,17 +21,19 @@ def _group(name, i, lr, betas=(0.9, 0.999), eps=1e-15):
             "name": name, "params": [i]}
 
 
-def _adam_state_dict(model, step):
+def _adam_state_dict(model, step, spatial_lr_scale=1.0):
     """train.TrainStep's Adam as a torch.optim.Adam state_dict (group order of the reference,
     gaussian_model.py:229-236).  The moments are stored in the shapes of the reference's parameter
     tensors (features_dc [N,1,C], features_rest [N,K-1,C], opacity [N,1]; gaussian_model.py:217-221),
     so the reference's own optimizer.load_state_dict + step accept them; TrainStep keeps flattened
     views of the same tensors.  Without a TrainStep a fresh state (no moments yet) is written, which
-    torch.optim.Adam.load_state_dict also accepts."""
+    torch.optim.Adam.load_state_dict also accepts; its mu group lr is position_lr_init *
+    spatial_lr_scale as training_setup sets it (gaussian_model.py:230), since load_state_dict copies the
+    saved group hyperparameters over the live ones."""
     if step is None:
         from .train import OptimizationParams
         o = OptimizationParams()
-        lrs = [o.position_lr_init, o.feature_lr, o.feature_lr / 20.0, o.opacity_lr, o.scaling_lr, o.rotation_lr]
+        lrs = [o.position_lr_init * float(spatial_lr_scale), o.feature_lr, o.feature_lr / 20.0, o.opacity_lr, o.scaling_lr, o.rotation_lr]
         return {"state": {}, "param_groups": [_group(n, i, lrs[i]) for i, n in enumerate(GROUP_ORDER)]}
     adam = step.adam
     lrs = step.learning_rates(step.iteration)
@@ -45,13 +47,16 @@ def _adam_state_dict(model, step):
     return {"state": state, "param_groups": groups}
 
 
-def save_checkpoint(path, model, train_step=None):
+def save_checkpoint(path, model, train_step=None, spatial_lr_scale=None):
     """torch.save of {mu, features_dc, features_rest, opacity, scaling, rotation, optimizer,
-    max_sh_degree, active_sh_degree} (+ 'iteration' when a TrainStep is given)."""
+    max_sh_degree, active_sh_degree} (+ 'iteration' when a TrainStep is given).  spatial_lr_scale
+    (default: the TrainStep's, else the model's attribute, else 1) scales the fresh mu group lr."""
+    if spatial_lr_scale is None:
+        spatial_lr_scale = getattr(train_step, "spatial_lr_scale", None) or getattr(model, "spatial_lr_scale", 1.0)
     ck = {k: getattr(model, "_" + k).detach().cpu() for k in PARAM_KEYS}
     ck["max_sh_degree"] = int(model.max_sh_degree)
     ck["active_sh_degree"] = int(model.active_sh_degree)
-    ck["optimizer"] = _adam_state_dict(model, train_step)
+    ck["optimizer"] = _adam_state_dict(model, train_step, spatial_lr_scale)
     if train_step is not None:
         ck["iteration"] = int(train_step.iteration)
     torch.save(ck, path)

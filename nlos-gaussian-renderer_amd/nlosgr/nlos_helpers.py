@@ -1,13 +1,21 @@
 """Drop-in counterparts of the reference's nlos_helpers.py hot-path functions, rendered by the
 HIP kernels (no dense [Ng, Na] torch tensors).
 
-    spherical_sample_histogram  nlos_helpers.py:124-188   (same return tuple)
-    gaussian_transient_rendering nlos_helpers.py:192-232  (same signature and outputs, real grads)
-    compute_loss                nlos_helpers.py:280-346   (same loss / equal_loss; no per-step .mat dump
-                                                           unless args.save_loss_mat is set)
-The default path T conventions apply (preset "torch"); args.occlusion selects the 'netf'
-self-transmittance model like gaussian_model.py:297-325.  args.render_cutoff (optional, default
-0 = dense, the reference's exact semantics) enables support culling at that Mahalanobis radius.
+    CUDA_AVAILABLE, CUDA_RENDERER          nlos_helpers.py:21-27       (created at import; None without a GPU)
+    spherical_sample_histogram             nlos_helpers.py:124-188     (same return tuple)
+    gaussian_transient_rendering           nlos_helpers.py:192-232     (same signature and outputs, real grads;
+                                                                        args.use_cuda_renderer dispatch :200-204)
+    gaussian_transient_rendering_cuda      nlos_helpers.py:235-278     (path C through GaussianRendererCUDA,
+                                                                        x Y^2 on both outputs)
+    compute_loss                           nlos_helpers.py:280-346     (same loss / equal_loss; no per-step .mat
+                                                                        dump unless args.save_loss_mat is set)
+Without args.use_cuda_renderer the default path T conventions apply (preset "torch"); args.occlusion
+selects the 'netf' self-transmittance model like gaussian_model.py:297-325.  args.render_cutoff
+(optional, default 0 = dense, the reference's exact semantics) enables support culling at that
+Mahalanobis radius.  With args.use_cuda_renderer set and a GPU present, rendering goes through path C
+(volume_renderer.cu conventions, shared transmittance when args.occlusion) exactly as the reference
+dispatches it; without a GPU the reference falls back to path T, and so does this module (whose
+path T then raises, since there is no CPU renderer).
 """
 import math
 
@@ -16,6 +24,10 @@ import torch
 from .geometry import geometry_from_ranges
 from .model import features_flat
 from .render import RenderConfig, render
+from .rendering_cuda import CUDA_AVAILABLE, create_cuda_renderer  # noqa: F401
+
+# nlos_helpers.py:21-27: the path-C renderer is created at import time (None when unavailable)
+CUDA_RENDERER = create_cuda_renderer()
 
 
 def cartesian2spherical_torch(pt):
@@ -80,7 +92,11 @@ def _mode(args):
 def gaussian_transient_rendering(args, model, data_kwargs, input_points, current_camera_grid_positions, I1, I2,
                                  num_r, dtheta, dphi):
     """(result [num_r, Ns^2], pred_histogram [num_r]) exactly as nlos_helpers.py:192-232 defines them,
-    with the dense Gaussian evaluation replaced by the HIP renderer."""
+    with the dense Gaussian evaluation replaced by the HIP renderer.  args.use_cuda_renderer routes to
+    gaussian_transient_rendering_cuda when the path-C renderer exists (:200-204)."""
+    if getattr(args, "use_cuda_renderer", False) and CUDA_RENDERER is not None:
+        return gaussian_transient_rendering_cuda(args, model, data_kwargs, input_points, current_camera_grid_positions,
+                                                 I1, I2, num_r, dtheta, dphi)
     ns = args.num_sampling_points
     dev = input_points.device
     c, deltaT = data_kwargs["c"], data_kwargs["deltaT"]
@@ -110,6 +126,33 @@ def gaussian_transient_rendering(args, model, data_kwargs, input_points, current
     result = result / (dist.view(-1, 1) ** 2) * torch.sin(Theta)
     result = result * (Y ** 2)
     return result, hist[0]
+
+
+def gaussian_transient_rendering_cuda(args, model, data_kwargs, input_points, current_camera_grid_positions, I1, I2,
+                                      num_r, dtheta, dphi):
+    """nlos_helpers.py:235-278: angular ranges recovered from input_points, r_range = (I1, I2) c dT,
+    GaussianRendererCUDA.render_transient (path C: ray grid, per-ray box filter, volume_renderer.cu
+    sampling, /(t^2 + 1e-8) sin(theta), angular sum), then x Y^2 on result and pred_histogram.
+    dtheta / dphi are recomputed by the renderer from the ranges, as in the reference."""
+    theta_vals = input_points[:, 3]
+    phi_vals = input_points[:, 4]
+    theta_min = theta_vals.min().item()
+    theta_max = theta_vals.max().item()
+    phi_min = phi_vals.min().item()
+    phi_max = phi_vals.max().item()
+    c, deltaT = data_kwargs["c"], data_kwargs["deltaT"]
+    r_min = I1 * c * deltaT
+    r_max = I2 * c * deltaT
+    result_3d, pred_histogram = CUDA_RENDERER.render_transient(
+        gaussian_model=model, camera_pos=current_camera_grid_positions, theta_range=(theta_min, theta_max),
+        phi_range=(phi_min, phi_max), r_range=(r_min, r_max), num_theta=args.num_sampling_points,
+        num_phi=args.num_sampling_points, num_r=num_r, c=c, deltaT=deltaT, scaling_modifier=args.scaling_modifier,
+        use_occlusion=args.occlusion, rendering_type=getattr(args, "rendering_type", "netf"))
+    result = result_3d.reshape(num_r, args.num_sampling_points * args.num_sampling_points)
+    Y = data_kwargs["volume_position"][1]
+    result = result * (Y ** 2)
+    pred_histogram = pred_histogram * (Y ** 2)
+    return result, pred_histogram
 
 
 def compute_loss(args, model, data_kwargs, optim_kwargs, device=None):

@@ -5,7 +5,11 @@
   <tag>_valu.json          SQ + GRBM pass: VALU issue utilisation = SQ_INSTS_VALU x 2 cycles per
                            wave64 instruction / (128 SIMDs per XCD x GRBM_GUI_ACTIVE), GRBM_GUI_ACTIVE
                            being the sum over the 8 XCDs of each XCD's busy cycles (so 1024 SIMDs x
-                           GRBM/8).  Transcendentals issue for longer, so this is a lower bound.
+                           GRBM/8).  The 2 cycles: MI355X_MICROARCH.md:54 ("issues each VALU
+                           instruction over 2 cycles (32 lanes/cycle x 2)") and :473 (v_fma_f32 wave64
+                           2 cyc on SIMD-32); measured here 2.6 for a v_fma_f32 chain incl. loop
+                           overhead, and 8.2 for v_exp_f32 (scripts/drain_proto.hip V0).  Every
+                           transcendental therefore issues 4x longer than this counts: a lower bound.
   <tag>_sq_counters.csv    the raw SQ/GRBM rows of this library's kernels (LDS pass counters merged
                            into <tag>_valu.json per kernel)
   <tag>_bench.json         the bench line of the same command, its roofline.traffic and VALU figure

@@ -213,3 +213,63 @@ def test_rays_backward_deterministic(occl):
     for a, b in zip(r1, r2):
         assert torch.isfinite(a).all()
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("occl", [False, True])
+def test_compute_loss_use_cuda_renderer(occl):
+    """nlos_helpers.compute_loss with args.use_cuda_renderer=True (nlos_helpers.py:200-204) takes
+    gaussian_transient_rendering_cuda (:235-278): path C via GaussianRendererCUDA with the angular
+    ranges recovered from input_points, r_range = (I1, I2) c dT and x Y^2 on result AND histogram.
+    Loss and all parameter gradients against the same composition on the oracle (render_rays_cuda
+    over the aabb_filter rows, CUDARenderModule's attenuation and angular sum)."""
+    from types import SimpleNamespace
+    from nlosgr import nlos_helpers as NH
+    from nlosgr.geometry import volume_box_point
+    from oracle import torch_ref as R
+    assert NH.CUDA_RENDERER is not None and NH.CUDA_AVAILABLE
+    dev = torch.device("cuda:0")
+    m, _, _ = _scene(70, 1, 51, scale_shift=1.0, opac_shift=4.0 if occl else 0.0, deg=0)
+    ns, T = 6, 40
+    c, deltaT = 1.0, 1.28 / T
+    start = T // 8
+    args = SimpleNamespace(num_sampling_points=ns, start=start, end=start + T, occlusion=occl, rendering_type="netf",
+                           scaling_modifier=1.0, gt_times=100, use_cuda_renderer=True)
+    walls = torch.tensor([[0.1, 0.0, -0.1], [-0.2, 0.0, 0.15]], device=dev)
+    vpos = torch.tensor([0.0, 0.5, 0.0], device=dev)
+    g = torch.Generator().manual_seed(3)
+    data_kwargs = {"nlos_data": (torch.rand(start + T + 2, 1, 2, generator=g) * 1e-3).to(dev),
+                   "camera_grid_positions": walls.t().contiguous(), "volume_position": vpos,
+                   "volume_box_point": volume_box_point(vpos, 0.5).to(dev), "deltaT": deltaT, "c": c}
+    crit = torch.nn.MSELoss(reduction="mean")
+    total = 0.0
+    P, _ = _oracle(m, 0)
+    ref_total = 0.0
+    for w in range(2):
+        loss, eq = NH.compute_loss(args, m, data_kwargs, {"m": 0, "N": 2, "n": w, "criterion": crit}, dev)
+        total = total + loss
+        # oracle composition (rendering_cuda.py:208-263 -> cuda_autograd.py:213-316, x Y^2)
+        cam = walls[w]
+        ip, I1, I2, num_r, *_ = NH.spherical_sample_histogram(args, data_kwargs, cam)
+        tr_ = (ip[:, 3].min().item(), ip[:, 3].max().item())
+        pr_ = (ip[:, 4].min().item(), ip[:, 4].max().item())
+        theta = torch.linspace(*tr_, ns)
+        phi = torch.linspace(*pr_, ns)
+        tg, pg = torch.meshgrid(theta, phi, indexing="ij")
+        tf, pf = tg.reshape(-1), pg.reshape(-1)
+        d = torch.stack([torch.sin(tf) * torch.cos(pf), torch.sin(tf) * torch.sin(pf), torch.cos(tf)], 1)
+        o = cam.cpu().unsqueeze(0).expand(tf.shape[0], 3).contiguous()
+        t = torch.linspace(I1 * c * deltaT, I2 * c * deltaT, num_r)
+        filt = R.aabb_filter(o, d, R.bboxes_cuda(P))
+        rho, _, _ = R.render_rays_cuda(o, d, t, P, P._features_dc[:, :, 0], cam.cpu(), 0, c, deltaT, 1.0, occl, filt)
+        res = rho.T.reshape(num_r, ns, ns) / (t.view(-1, 1, 1) ** 2 + 1e-8) * torch.sin(tg.unsqueeze(0))
+        hist = res.sum(dim=(1, 2)) * ((tr_[1] - tr_[0]) / ns) * ((pr_[1] - pr_[0]) / ns) * (0.5 ** 2)
+        target = data_kwargs["nlos_data"][I1:I1 + num_r, 0, w].cpu() * 100
+        ref_loss = crit(hist, target)
+        np.testing.assert_allclose(loss.item(), ref_loss.item(), rtol=(4e-4 if occl else 4e-5))
+        ref_total = ref_total + ref_loss
+    total.backward()
+    ref_total.backward()
+    for name, leaf, rleaf in [("mu", m._mu, P._mu), ("scaling", m._scaling, P._scaling),
+                              ("rotation", m._rotation, P._rotation), ("opacity", m._opacity, P._opacity),
+                              ("features_dc", m._features_dc, P._features_dc)]:
+        _close(leaf.grad, rleaf.grad, 3e-4 if occl else 2e-4, atol=1e-6, msg=f"grad {name}")

@@ -68,6 +68,22 @@ def test_checkpoint_optimizer_loads_into_reference_adam(tmp_path, with_step):
     assert all(torch.isfinite(t).all() for t in leaves)
 
 
+def test_checkpoint_fresh_state_mu_lr_has_spatial_scale(tmp_path):
+    """Without a TrainStep the saved mu group lr is position_lr_init * spatial_lr_scale, as
+    training_setup sets it (gaussian_model.py:230); Adam.load_state_dict copies it over the live one."""
+    from nlosgr.checkpoint import save_checkpoint
+    from nlosgr.model import GaussianParams
+    from nlosgr.train import OptimizationParams
+    p = _ref_params(5, 16)
+    m = GaussianParams(p["mu"], p["scaling"], p["rotation"], p["opacity"], p["features_dc"], p["features_rest"], 3, 3)
+    f = tmp_path / "ck.pt"
+    save_checkpoint(str(f), m, None, spatial_lr_scale=2.5)
+    ck = torch.load(str(f), weights_only=True)
+    lr = ck["optimizer"]["param_groups"][0]["lr"]
+    assert ck["optimizer"]["param_groups"][0]["name"] == "mu"
+    assert abs(lr - OptimizationParams().position_lr_init * 2.5) < 1e-12
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
