@@ -76,6 +76,14 @@ class Geometry:
                         self.cos_phi[a:b], self.grid_lin[a:b], self.hscale[a:b], self.r, self.att,
                         self.theta[a:b], self.phi[a:b], self.nt, self.np, self.nr)
 
+    def rows(self, idx):
+        """Wall points idx (int64, e.g. distributed.wall_rows: the row-interleaved shard bench.py uses)."""
+        idx = idx.to(self.wall.device)
+        pick = lambda t: t.index_select(0, idx).contiguous()
+        return Geometry(pick(self.wall), pick(self.sin_theta), pick(self.cos_theta), pick(self.sin_phi),
+                        pick(self.cos_phi), pick(self.grid_lin), pick(self.hscale), self.r, self.att,
+                        pick(self.theta), pick(self.phi), self.nt, self.np, self.nr)
+
 
 def radial_tables(start, end, c, deltaT, preset, device):
     """r_k and the per-bin attenuation.

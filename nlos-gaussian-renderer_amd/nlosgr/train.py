@@ -187,8 +187,10 @@ class TrainStep:
     """
 
     def __init__(self, model, geo, cfg, target, gt_times=1.0, opt=None, spatial_lr_scale=1.0, nwall_total=None,
-                 group=None, sh_schedule=False, events=None, buckets=4):
+                 group=None, sh_schedule=False, events=None, buckets=4, keep_grads=False):
         self.model, self.geo, self.cfg = model, geo, cfg
+        self.keep_grads = keep_grads   # tests: keep the last step's (all-reduced) gradients in self.grads
+        self.grads = None
         self.target = target.detach().float().contiguous()
         self.gt_times = float(gt_times)
         self.opt = opt or OptimizationParams()
@@ -292,6 +294,8 @@ class TrainStep:
             grads[4] = grads[4] + (self.opt.scale_reg / es.numel()) * es
             reg = self.opt.opacity_reg * so.mean() + self.opt.scale_reg * es.mean()
             loss2 = torch.stack([loss2[0] + reg, loss2[1]])
+        if self.keep_grads:
+            self.grads = [g.clone() for g in grads]
         self.adam.step(grads, self.learning_rates(it))
         self.iteration = it + 1
         if self.sh_schedule and self.iteration % 1000:   # main.py:240-241 (fires when NOT a multiple)

@@ -527,3 +527,64 @@ def render_rays_analytic(ray_o, ray_d, t_min, t_max, filt, P, sh_features, cam, 
                 break
         out[ray] = acc
     return out
+
+
+def render_rays_analytic_batched(ray_o, ray_d, t_min, t_max, filt, P, sh_features, cam, deg, mod=1.0, sigma=3.0,
+                                 chunk=2048):
+    """render_rays_analytic (above, the line-by-line restatement of volume_renderer_analytic.cu:23-173)
+    vectorised over rays and filter entries, for the C4-size cross-check of path A (test
+    infrastructure; pinned to the loop version by tests/test_oracle_analytic_cpu.py).  Same rules:
+    the first 128 filter entries (filter order) whose sigma-ellipsoid section is non-empty after the
+    [t_min, t_max] clip, stable sort by t_enter, tau clamped >= 0, front-to-back compositing that
+    stops once T < 1e-4 (a section contributes iff the transmittance before it is >= 1e-4)."""
+    ng = P._mu.shape[0]
+    s_all = torch.exp(P._scaling) * mod
+    R_all = quat_to_rotmat_cuda(P._rotation)
+    sig_all = torch.sigmoid(P._opacity).reshape(-1)
+    d = P._mu - cam[None, :]
+    dn = d * (1.0 / (torch.sqrt((d * d).sum(dim=1, keepdim=True)) + 1e-8))
+    rho_all = torch.clamp_min(eval_sh_cuda(deg, sh_features, dn) + 0.5, 0.0).reshape(-1)
+    out = torch.zeros(ray_o.shape[0])
+    ne = filt.shape[1] - 1
+    for r0 in range(0, ray_o.shape[0], chunk):
+        o = ray_o[r0:r0 + chunk]
+        dv = ray_d[r0:r0 + chunk]
+        f = filt[r0:r0 + chunk]
+        n = f[:, 0:1].long()
+        gi = f[:, 1:].long()
+        ent = torch.arange(ne).view(1, -1)
+        ok = (ent < n) & (gi >= 0) & (gi < ng)
+        g = torch.where(ok, gi, torch.zeros_like(gi))
+        Rt = R_all[g].transpose(-1, -2)                                    # [n, ne, 3, 3]
+        so = (Rt @ (o[:, None, :] - P._mu[g]).unsqueeze(-1)).squeeze(-1) / s_all[g]
+        sd = (Rt @ dv[:, None, :].expand(-1, ne, -1).unsqueeze(-1)).squeeze(-1) / s_all[g]
+        a = (sd * sd).sum(-1)
+        b = 2.0 * (so * sd).sum(-1)
+        cc = (so * so).sum(-1) - sigma * sigma
+        disc = b * b - 4.0 * a * cc
+        sq = torch.sqrt(torch.clamp_min(disc, 0.0))
+        te = torch.clamp_min((-b - sq) / (2.0 * a), t_min)
+        tx = torch.clamp_max((-b + sq) / (2.0 * a), t_max)
+        sec = ok & (disc >= 0) & (te < tx)
+        sec = sec & (torch.cumsum(sec.long(), dim=1) <= 128)               # the 128-section cap
+        key = torch.where(sec, te, torch.full_like(te, float("inf")))
+        order = torch.sort(key, dim=1, stable=True).indices
+        take = lambda t: torch.gather(t, 1, order)
+        sec_s = take(sec)
+        A = take((so * so).sum(-1))
+        B = take(b)
+        C = take(a)
+        gs = take(g)
+        te_s, tx_s = take(te), take(tx)
+        G = sig_all[gs] * torch.sqrt(2.0 * math.pi / C) * s_all[gs].prod(-1)
+        ef = torch.exp(-0.5 * (A - B * B / (4.0 * C)))
+        e1 = torch.special.erf((B + 2.0 * C * tx_s) / (2.0 * torch.sqrt(C)))
+        e0 = torch.special.erf((B + 2.0 * C * te_s) / (2.0 * torch.sqrt(C)))
+        tau = torch.where(sec_s, torch.clamp_min(G * ef * (e1 - e0), 0.0), torch.zeros_like(A))
+        st = torch.exp(-tau)
+        T_incl = torch.cumprod(st, dim=1)
+        T_excl = torch.cat([torch.ones_like(T_incl[:, :1]), T_incl[:, :-1]], dim=1)
+        live = sec_s & (T_excl >= 1e-4)
+        contrib = torch.where(live, T_excl * (1.0 - st) * rho_all[gs], torch.zeros_like(A))
+        out[r0:r0 + chunk] = torch.cumsum(contrib, dim=1)[:, -1]
+    return out

@@ -166,3 +166,42 @@ def test_binint_vs_numerical_crosscheck():
     s_min = torch.exp(m._scaling).min().item()
     bound = 4 * (dr / s_min) ** 2 / 24
     assert 0 < rel < bound, (rel, bound)
+
+
+def test_path_a_at_c4_scale():
+    """Path A (nlosgr_rays_analytic = _C.render_rays_analytic, volume_renderer_analytic.cu:23-241) on
+    the C3/C4 inputs: all 100k Gaussians, the full 32x32 ray grids of 4 wall points (angular ranges
+    of spherical_sample_histogram, t range (I1, I2) c dT), per-ray 3-sigma box filter with the
+    256-entry cap, 128-section cap, early exit.  Every ray's value against the vectorised oracle
+    restatement fed the same filter rows (the filter itself is bit-exact vs the oracle's, see
+    test_gpu_rays.py::test_filter_matches_oracle)."""
+    from nlosgr import GaussianParams, features_flat
+    from nlosgr.rays import filter_gaussians_per_ray, render_rays_analytic
+    from nlosgr.render import bboxes
+    from nlosgr.volume import Scene
+    from oracle import torch_ref as R
+    dev = torch.device("cuda:0")
+    scene = Scene(H=128, W=128, T=1024, ns=32)
+    m = GaussianParams.synthetic(100_000, 3, preset="cuda", device=dev, seed=0)
+    geo = scene.geometry(dev, "cuda", "noocl")
+    feats = features_flat(m)
+    bb = bboxes(m._mu, m._scaling, m._rotation, 1.0, 3.0, preset="torch").view(-1, 6)
+    P = _oracle_params(m, 3)
+    t0, t1 = float(geo.r[0]), float(geo.r[-1])
+    capped = 0
+    for p in (0, 128 * 40 + 30, 128 * 64 + 64, 128 * 127 + 100):
+        th, ph = geo.theta[p], geo.phi[p]
+        tg, pg = torch.meshgrid(th, ph, indexing="ij")
+        tf, pf = tg.reshape(-1), pg.reshape(-1)
+        d = torch.stack([torch.sin(tf) * torch.cos(pf), torch.sin(tf) * torch.sin(pf), torch.cos(tf)], 1).contiguous()
+        cam = geo.wall[p].contiguous()
+        o = cam.unsqueeze(0).expand(d.shape[0], 3).contiguous()
+        filt = filter_gaussians_per_ray(o, d, m._mu, bb, 3.0)
+        out = render_rays_analytic(o, d, t0, t1, filt, m._mu, m._scaling, m._rotation, m._opacity, feats, cam, 3,
+                                   1.0, 1.28 / 1024, 1.0, 3.0)
+        assert out.shape == (1024,) and torch.isfinite(out).all()
+        capped += int((filt[:, 0] >= 256).sum())
+        ref = R.render_rays_analytic_batched(o.cpu(), d.cpu(), t0, t1, filt.cpu(), P, feats.detach().cpu(), cam.cpu(), 3)
+        assert ref.abs().max() > 0
+        _close(out.cpu(), ref, 1e-5, 1e-7, f"path A wall point {p}")
+    assert capped > 0   # the reference's 256-entry truncation is exercised at this density

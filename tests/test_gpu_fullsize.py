@@ -199,29 +199,68 @@ def test_c4_full_size_binint_vs_numerical():
     assert rel < 1e-3, f"binint vs numerical rel-L2 {rel:.3e}"
 
 
-def test_c5_band_full_size():
-    """C5 (500k Gaussians -> 256x256 wall x 2048 bins) is an 8-GPU config: one rank's band (1/8 of
-    the wall) at full size, forward at 5.7 sigma, finite; one wall point vs the dense HIP evaluation;
-    a Gaussian subset vs the oracle on 1 wall point."""
+def test_c5_rows_shard_train_step():
+    """C5 (500k Gaussians -> 256x256 wall x 2048 bins) is the 8-GPU config: one rank's shard exactly as
+    bench.py --gpus 8 runs it (wall_rows(256, 256, 3, 8): whole rows 3, 11, ..., 8192 wall points),
+    cutoff 5.7 sigma, through the full TrainStep (forward + MSE over the whole volume's normaliser +
+    backward of all six raw tensors + Adam).  Checks: the shard's forward volume, the step's loss, all
+    gradients and all updated parameters are finite; 2 sampled wall points of the shard vs the dense
+    HIP evaluation, histogram and gradients seeded there (same culled kernels as the step); a Gaussian
+    subset vs the oracle on one wall point of the shard."""
     from nlosgr import GaussianParams
-    from nlosgr.distributed import wall_band
-    from nlosgr.render import render_forward
+    from nlosgr.distributed import wall_rows
+    from nlosgr.render import render_backward, render_forward
+    from nlosgr.train import TrainStep
     from nlosgr.volume import Scene, make_config
     dev = torch.device("cuda:0")
-    scene = Scene(H=256, W=256, T=2048, ns=32)
+    H = W = 256
+    T = 2048
+    scene = Scene(H=H, W=W, T=T, ns=32)
     m = GaussianParams.synthetic(500_000, 3, preset="cuda", device=dev, seed=0)
-    b0, b1 = wall_band(256 * 256, 3, 8)
-    walls = scene.walls(dev)[b0:b1].contiguous()
-    geo = scene.geometry(dev, "cuda", "noocl", walls=walls)
+    rows = wall_rows(H, W, 3, 8, device=dev)
+    assert rows.numel() == 8192
+    geo = scene.geometry(dev, "cuda", "noocl").rows(rows)
     cfg = make_config(m, scene, "cuda", "noocl", cutoff=PARITY_CUTOFF)
     hist, _ = render_forward(*_params(m), geo, cfg)
-    assert hist.shape == (b1 - b0, 2048)
+    assert hist.shape == (8192, T)
     _finite_volume(hist)
-    k = 4000
-    gdense = scene.geometry(dev, "cuda", "noocl", walls=walls[k:k + 1].contiguous())
-    ref, _ = render_forward(*_params(m), gdense, make_config(m, scene, "cuda", "noocl", cutoff=0.0))
-    _close(hist[k:k + 1], ref, 1e-5, msg="C5 band culled vs dense")
+    idx = torch.tensor([700, 6000], device=dev)
+    wsel = geo.wall[idx].contiguous()
+    # culled (full shard) vs dense HIP on the sampled wall points: histogram, then gradients seeded there
+    gd = scene.geometry(dev, "cuda", "noocl", walls=wsel)
+    dcfg = make_config(m, scene, "cuda", "noocl", cutoff=0.0)
+    ref, _ = render_forward(*_params(m), gd, dcfg)
+    _close(hist[idx], ref, 1e-5, msg="C5 shard culled vs dense hist")
+    g = torch.Generator().manual_seed(5)
+    gseed = torch.randn(len(idx), T, generator=g).to(dev)
+    gfull = torch.zeros(8192, T, device=dev)
+    gfull[idx] = gseed
+    d = render_backward(*_params(m), geo, cfg, grad_hist=gfull)
+    dref = render_backward(*_params(m), gd, dcfg, grad_hist=gseed)
+    for name, a, b in zip(("mu", "scaling", "rotation", "opacity", "features"), d, dref):
+        assert torch.isfinite(a).all()
+        _close(a, b, 2e-4, atol=1e-9, msg=f"C5 shard culled vs dense grad {name}")
+    del d, dref, gfull
+    # a Gaussian subset on the shard's geometry against the oracle (same support rule)
     sub = _subset(m, torch.arange(0, 500_000, 5000, device=dev))
-    hs, _ = render_forward(*_params(sub), gdense, make_config(sub, scene, "cuda", "noocl", cutoff=PARITY_CUTOFF))
-    ref, _ = _oracle(sub, scene, torch.tensor([b0 + k]), "cuda", "noocl", PARITY_CUTOFF)
+    g1 = scene.geometry(dev, "cuda", "noocl", walls=wsel[:1].contiguous())
+    hs, _ = render_forward(*_params(sub), g1, make_config(sub, scene, "cuda", "noocl", cutoff=PARITY_CUTOFF))
+    ref, _ = _oracle(sub, scene, rows[idx[:1]].cpu(), "cuda", "noocl", PARITY_CUTOFF)
     _close(hs, ref, 2e-5, msg="C5 subset hist")
+    # the step itself: TrainStep on the shard (normaliser of the whole 256x256 volume)
+    gt = torch.Generator().manual_seed(1)
+    target = (torch.rand(8192, T, generator=gt) * 1e-3).to(dev)
+    step = TrainStep(m, geo, cfg, target, gt_times=100.0, nwall_total=H * W, keep_grads=True)
+    before = [p.detach().clone() for p in m.parameters()]
+    loss2 = step()
+    torch.cuda.synchronize()
+    assert torch.isfinite(loss2).all() and float(loss2[0]) > 0
+    # the step's MSE (single process: this shard's mean; its gradient carries n_shard / n_volume)
+    se = ((hist.double() - target.double() * 100.0) ** 2).mean()
+    assert abs(float(loss2[0]) - float(se)) <= 1e-4 * float(se)
+    for gr in step.grads:
+        assert torch.isfinite(gr).all()
+    assert float(step.grads[0].abs().max()) > 0
+    for b, p in zip(before, m.parameters()):
+        assert torch.isfinite(p).all()
+    assert not torch.equal(before[0], m._mu.detach())

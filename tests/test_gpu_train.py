@@ -238,12 +238,12 @@ def _shard_worker(rank, world, port, out):
     os.environ["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        from nlosgr.distributed import wall_band
+        from nlosgr.distributed import wall_rows
         from nlosgr.train import TrainStep
         dev = torch.device("cuda:0")
         scene, model, geo, cfg, target = _scene_model(dev, ng=1500)
-        b0, b1 = wall_band(geo.nwall, rank, world)
-        step = TrainStep(model, geo.slice(b0, b1), cfg, target[b0:b1].contiguous(), gt_times=100.0, buckets=4)
+        idx = wall_rows(scene.H, scene.W, rank, world, device=dev)   # the split bench.py --gpus N uses
+        step = TrainStep(model, geo.rows(idx), cfg, target[idx].contiguous(), gt_times=100.0, buckets=4)
         losses = [step(it).cpu() for it in range(2)]
         torch.cuda.synchronize()
         out[rank] = ([p.detach().cpu() for p in model.parameters()], losses)
@@ -252,8 +252,9 @@ def _shard_worker(rank, world, port, out):
 
 
 def test_sharded_train_step_matches_single_process():
-    """Two gloo ranks sharing the GPU, each training its wall band (bucketed, overlapped gradient
-    all-reduce, TrainStep.buckets = 4) == one process training the whole wall."""
+    """Two gloo ranks sharing the GPU, each training its row-interleaved wall shard (wall_rows, as
+    bench.py --gpus N shards; bucketed, overlapped gradient all-reduce, TrainStep.buckets = 4) ==
+    one process training the whole wall."""
     import socket
     import torch.multiprocessing as mp
     from nlosgr.train import TrainStep
@@ -275,3 +276,52 @@ def test_sharded_train_step_matches_single_process():
             # band sums add in another order: Adam's first steps ~ lr sign(g) can flip a near-zero gradient
             bad = ((a - b.detach().cpu()).abs() > 1e-5 * (1 + b.detach().cpu().abs())).float().mean().item()
             assert bad < 2e-3, (n, bad)
+
+
+def _rccl_worker(rank, world, port, out):
+    import os
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    os.environ["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=rank, world_size=world)   # RCCL on ROCm
+    try:
+        from nlosgr.train import BucketedAllReduce, allreduce_step, bucket_bounds
+        dev = torch.device("cuda:0")
+        g = torch.Generator().manual_seed(2)
+        ng = 1300
+        grads = [torch.randn(ng, 3, generator=g).to(dev), torch.randn(ng, 1, generator=g).to(dev),
+                 torch.randn(ng, 15, generator=g).to(dev), torch.randn(ng, generator=g).to(dev),
+                 torch.randn(ng, 3, generator=g).to(dev), torch.randn(ng, 4, generator=g).to(dev)]
+        ref = [t.clone() for t in grads]
+        loss4 = torch.tensor([0.5, 2.0, 10.0, 5.0], device=dev)
+        out_g, loss2 = allreduce_step([t.clone() for t in grads], loss4, 20)
+        ex = BucketedAllReduce([t.clone() for t in grads], bucket_bounds(ng, 4), None)
+        for b in range(len(bucket_bounds(ng, 4))):
+            ex.launch(b)
+        bucketed = ex.finish()
+        torch.cuda.synchronize()
+        out[rank] = ([t.cpu() for t in ref], [t.cpu() for t in out_g], [t.cpu() for t in bucketed], loss2.cpu())
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rccl_exchange_single_rank():
+    """The gradient exchange on the RCCL ("nccl") backend itself, on device buffers: the packed
+    all-reduce (allreduce_step) and the bucketed overlapped one (BucketedAllReduce) on a one-rank
+    group return the inputs unchanged and the global loss (sum of squared errors / n, se / st).
+    One GPU cannot host two RCCL ranks (duplicate device), so the two-rank exchange is covered on
+    gloo (test_sharded_train_step_matches_single_process, tests/test_step_exchange_cpu.py)."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    out = mp.Manager().dict()
+    mp.spawn(_rccl_worker, args=(1, port, out), nprocs=1, join=True)
+    ref, got, bucketed, loss2 = out[0]
+    for a, b, c in zip(ref, got, bucketed):
+        assert torch.equal(a, b) and torch.equal(a, c)
+    torch.testing.assert_close(loss2, torch.tensor([0.5, 2.0]))

@@ -140,3 +140,31 @@ def test_bin_integral_matches_quadrature():
         acc /= sub.shape[0]
         err = (exact - acc).abs().max().item() / acc.abs().max().item()
         assert err < 1e-6, (preset, err)
+
+
+def test_batched_analytic_matches_loop():
+    """The vectorised analytic oracle (used for the C4-size path-A check on the GPU) equals the
+    line-by-line restatement on random scenes with the 128-section cap, the 256-entry filter cap,
+    -1 padding and early exits."""
+    from oracle import torch_ref as R
+    g = torch.Generator().manual_seed(4)
+    for ng, shift, opac in ((40, 0.5, 0.0), (300, 1.8, 1.5), (30, 2.5, 6.0)):
+        mu = torch.rand(ng, 3, generator=g) * 0.4 + torch.tensor([-0.2, 0.3, -0.2])
+        S = torch.log(torch.full((ng, 3), 0.04)) + 0.3 * torch.randn(ng, 3, generator=g) + shift
+        q = torch.randn(ng, 4, generator=g)
+        o = torch.randn(ng, 1, generator=g) + opac
+        dc = torch.rand(ng, 1, 1, generator=g) * 0.4 - 0.2
+        rest = 0.05 * torch.randn(ng, 3, 1, generator=g)
+        P = R.Params(mu, S, q, o, dc, rest, 1, requires_grad=False)
+        feats = torch.cat([dc, rest], dim=1)[:, :, 0]
+        nr = 24
+        th = 0.4 + torch.rand(nr, generator=g)
+        ph = 1.0 + torch.rand(nr, generator=g)
+        d = torch.stack([torch.sin(th) * torch.cos(ph), torch.sin(th) * torch.sin(ph), torch.cos(th)], 1)
+        cam = torch.tensor([0.02, 0.0, -0.03])
+        ray_o = cam.unsqueeze(0).expand(nr, 3).contiguous()
+        filt = R.aabb_filter(ray_o, d, R.bboxes_cuda(P))
+        loop = R.render_rays_analytic(ray_o, d, 0.16, 1.44, filt, P, feats, cam, 1)
+        vec = R.render_rays_analytic_batched(ray_o, d, 0.16, 1.44, filt, P, feats, cam, 1, chunk=7)
+        assert loop.abs().max() > 0
+        assert torch.allclose(vec, loop, rtol=1e-5, atol=1e-7), (ng, (vec - loop).abs().max())
