@@ -530,13 +530,22 @@ def render_rays_analytic(ray_o, ray_d, t_min, t_max, filt, P, sh_features, cam, 
 
 
 def render_rays_analytic_batched(ray_o, ray_d, t_min, t_max, filt, P, sh_features, cam, deg, mod=1.0, sigma=3.0,
-                                 chunk=2048):
+                                 chunk=2048, dtype=None):
     """render_rays_analytic (above, the line-by-line restatement of volume_renderer_analytic.cu:23-173)
     vectorised over rays and filter entries, for the C4-size cross-check of path A (test
     infrastructure; pinned to the loop version by tests/test_oracle_analytic_cpu.py).  Same rules:
     the first 128 filter entries (filter order) whose sigma-ellipsoid section is non-empty after the
     [t_min, t_max] clip, stable sort by t_enter, tau clamped >= 0, front-to-back compositing that
-    stops once T < 1e-4 (a section contributes iff the transmittance before it is >= 1e-4)."""
+    stops once T < 1e-4 (a section contributes iff the transmittance before it is >= 1e-4).
+    dtype=torch.float64 evaluates the same formula in double precision: with small Gaussians tau is
+    ~1e-7 and the reference's fp32 1 - exp(-tau) is all cancellation, so parity is judged against
+    the formula's exact value (the HIP kernel evaluates 1 - exp(-tau) as -expm1(-tau))."""
+    if dtype is not None:
+        from types import SimpleNamespace
+        cv = lambda t: t.to(dtype)
+        P = SimpleNamespace(_mu=cv(P._mu), _scaling=cv(P._scaling), _rotation=cv(P._rotation),
+                            _opacity=cv(P._opacity))
+        ray_o, ray_d, sh_features, cam = cv(ray_o), cv(ray_d), cv(sh_features), cv(cam)
     ng = P._mu.shape[0]
     s_all = torch.exp(P._scaling) * mod
     R_all = quat_to_rotmat_cuda(P._rotation)
@@ -544,7 +553,7 @@ def render_rays_analytic_batched(ray_o, ray_d, t_min, t_max, filt, P, sh_feature
     d = P._mu - cam[None, :]
     dn = d * (1.0 / (torch.sqrt((d * d).sum(dim=1, keepdim=True)) + 1e-8))
     rho_all = torch.clamp_min(eval_sh_cuda(deg, sh_features, dn) + 0.5, 0.0).reshape(-1)
-    out = torch.zeros(ray_o.shape[0])
+    out = torch.zeros(ray_o.shape[0], dtype=ray_o.dtype)
     ne = filt.shape[1] - 1
     for r0 in range(0, ray_o.shape[0], chunk):
         o = ray_o[r0:r0 + chunk]
