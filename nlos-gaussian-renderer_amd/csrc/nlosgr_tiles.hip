@@ -115,6 +115,14 @@ __device__ __forceinline__ float quadric(const float* M, float dx, float dy, flo
     return fmaf(dx, t0, fmaf(dy, t1, dz * dz * M[5]));
 }
 
+// 1 - exp(-x) for 0 <= x <= 1/64 (x = sigma pdf c dT <= c dT): x (1 - x/2 + x^2/6 - x^3/24), truncation
+// x^4/120 <= 5e-10 relative.  Used instead of an exp (and of its cancelling 1 - exp) when c dT <= 1/64
+// (C3: c dT = 1.25e-3), which makes the whole launch take the polynomial (a kernel-uniform branch).
+constexpr float kSmallX = 1.0f / 64.0f;
+__device__ __forceinline__ float om_exp_small(float x) {
+    return x * fmaf(x, fmaf(x, fmaf(x, -1.0f / 24.0f, 1.0f / 6.0f), -0.5f), 1.0f);
+}
+
 // value of lane s (wave-uniform s) as a scalar
 __device__ __forceinline__ float rlf(float v, int s) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), s));
@@ -222,6 +230,7 @@ __global__ __launch_bounds__(tile_threads<BWD>()) void tile_kernel(TArgs k) {
     const float inv_dr = 1.0f / dr;
     const float cdt = k.opt.c_deltaT;
     const float ncdt = -cdt * kLog2e;   // exp(-x c dT) = exp2(x ncdt)
+    const bool small_x = cdt <= kSmallX;  // 1 - exp(-sigma pdf c dT) by om_exp_small
     const int nch = (nr + 63) / 64;
     const int deg = k.g.sh_degree, K = (deg + 1) * (deg + 1);
 
@@ -287,7 +296,8 @@ __global__ __launch_bounds__(tile_threads<BWD>()) void tile_kernel(TArgs k) {
                 __syncthreads();
             }
             int qn = 0;
-            for (int g0 = 0; !skip0 && (g0 < k.g.ng || qn > 0); g0 += kTB) {
+            bool capped = false;   // AABB: every ray of the tile holds its 256 selections (nothing later counts)
+            for (int g0 = 0; !skip0 && !capped && (g0 < k.g.ng || qn > 0); g0 += kTB) {
                 // ---- cull round: lane = Gaussian, 512 per round, ordered append ----
                 if (g0 < k.g.ng) {
                     const int gi = g0 + tid;
@@ -448,7 +458,8 @@ __global__ __launch_bounds__(tile_threads<BWD>()) void tile_kernel(TArgs k) {
                                             const float cv = (unsigned)(kb - skl) <= (unsigned)slen ? e0.w * pdf : 0.f;
                                             if (OCCL) {
                                                 accD += cv;
-                                                accW = fmaf(e1.x, 1.0f - fast_exp2(cv * ncdt), accW);
+                                                const float w = small_x ? om_exp_small(cv * cdt) : 1.0f - fast_exp2(cv * ncdt);
+                                                accW = fmaf(e1.x, w, accW);
                                             } else {
                                                 accW = fmaf(e1.x, cv, accW);
                                             }
@@ -596,9 +607,10 @@ __global__ __launch_bounds__(tile_threads<BWD>()) void tile_kernel(TArgs k) {
                                     ab1 = row[kb + 2];
                                     float dc;
                                     if (OCCL) {
-                                        const float ex = fast_exp2(cv * ncdt);
+                                        const float om = small_x ? om_exp_small(cv * cdt) : 1.0f - fast_exp2(cv * ncdt);
+                                        const float ex = 1.0f - om;
                                         dc = fmaf(ab.x * rc, ex, ab.y);
-                                        pr = fmaf(ab.x, 1.0f - ex, pr);
+                                        pr = fmaf(ab.x, om, pr);
                                     } else {
                                         dc = ab.x * wrho;
                                         pr = fmaf(ab.x, cv, pr);
@@ -735,6 +747,20 @@ __global__ __launch_bounds__(tile_threads<BWD>()) void tile_kernel(TArgs k) {
                     qn = rest;
                     __syncthreads();
                     TDIAG(trays)
+                    if (SEL == NLOSGR_SELECT_AABB) {
+                        // the filter keeps the first 256 box hits by index per ray (ray_aabb.cu:10-61) and
+                        // windows arrive in index order: once every ray of the tile is full, stop
+                        bool full = true;
+                        for (int r = 0; r < RT; ++r) {
+                            const int i = ti0 + r / k.tj, j = tj0 + r % k.tj;
+                            if (i < nt && j < np_ && icnt[r] < kCap) full = false;
+                        }
+                        if (full) {
+                            capped = true;
+                            qn = 0;
+                            break;
+                        }
+                    }
                 }
             }
 

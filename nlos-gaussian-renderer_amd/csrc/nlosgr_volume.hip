@@ -1003,7 +1003,11 @@ __device__ __forceinline__ bool bray_setup(const float* pd, float2 th, float2 ph
     return true;
 }
 
-template <int PRESET, int MODE, bool DENSE, bool RAYS, bool CACHE, bool SHR>
+// TAIL (culled no-occlusion histogram backward at cutoff >= kTailCutoff): the drain reads the upstream
+// row without the segment-end mask, see BV below
+constexpr float kTailCutoff = 5.0f;
+
+template <int PRESET, int MODE, bool DENSE, bool RAYS, bool CACHE, bool SHR, bool TAIL = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) void bwd_kernel(KArgs k) {
     extern __shared__ __align__(16) float smem[];
     const int nr = k.geo.nr, nt = k.geo.nt, np_ = k.geo.np, P_ = k.geo.nwall;
@@ -1186,7 +1190,20 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
                 const float* gw = RAYS && gray ? gray + (size_t)((b.ij & 0xFFFF) * np_ + (b.ij >> 16)) * nr + b.pos
                                                : nullptr;
                 float Hs[kBSteps];
-                if (BV) {
+                if (BV && TAIL) {
+                    // no end mask: a segment's last round also weighs the bins past its end (up to
+                    // kBSteps - 1 of them) with their exact pdf, < exp(-m_c^2 / 2) of the Gaussian's peak
+                    // (<= 3.7e-6 at m_c >= kTailCutoff: the support is a superset of the forward's, closer
+                    // to the dense reference; idle and blocked lanes are zeroed through their pdf seed
+                    // below).  Slot 0 before pos (o = 1) stays masked: the recurrence starts at pos.
+                    const float2* g2 = reinterpret_cast<const float2*>(gr);
+#pragma unroll
+                    for (int m = 0; m < kBSteps; m += 2) {
+                        const float2 h = g2[m / 2];
+                        Hs[m] = (m == 0 && o) ? 0.f : h.x;
+                        Hs[m + 1] = h.y;
+                    }
+                } else if (BV) {
                     const int lim = remw + o;
                     const float2* g2 = reinterpret_cast<const float2*>(gr);
 #pragma unroll
@@ -1211,6 +1228,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
                         // exp2 recurrence (kRecurrence) and moments about the round's first bin:
                         // U_n = sum_m hp m^n, then S_n += sum_m hp (kap + m)^n
                         float pdf = fast_exp2(fmaf(b.c2, kap * kap, b.c0));
+                        // BV reads the row unmasked: idle lanes and blocked ones (finished, rem <= 0, waiting
+                        // for their hand-off) contribute through a zero seed
+                        if (BV && TAIL && !(act && b.rem > 0)) pdf = 0.f;
                         float q = fast_exp2(b.c2 * fmaf(2.f, kap, 1.f));
                         const float cc = fast_exp2(2.f * b.c2);
                         float U0 = 0.f, U1 = 0.f, U2 = 0.f;
@@ -1580,10 +1600,15 @@ template <int PRESET, int MODE, bool DENSE, bool RAYS, bool CACHE>
 void launch_bwd(const KArgs& ka, size_t shm, hipStream_t s) {
     const int gpb = ka.bshared ? kNB * kWaves : kNB;
     dim3 grid((ka.g_hi - ka.g_lo + gpb - 1) / gpb, ka.nsplit);
-    if (ka.bshared)
-        hipLaunchKernelGGL((bwd_kernel<PRESET, MODE, DENSE, RAYS, CACHE, true>), grid, dim3(kBlock), shm, s, ka);
-    else
-        hipLaunchKernelGGL((bwd_kernel<PRESET, MODE, DENSE, RAYS, CACHE, false>), grid, dim3(kBlock), shm, s, ka);
+    constexpr bool kCanTail = MODE == NLOSGR_MODE_NOOCL && !DENSE && !RAYS;
+    const bool tail = kCanTail && ka.opt.cutoff >= kTailCutoff;
+    if (ka.bshared) {
+        if (tail) hipLaunchKernelGGL((bwd_kernel<PRESET, MODE, DENSE, RAYS, CACHE, true, kCanTail>), grid, dim3(kBlock), shm, s, ka);
+        else hipLaunchKernelGGL((bwd_kernel<PRESET, MODE, DENSE, RAYS, CACHE, true>), grid, dim3(kBlock), shm, s, ka);
+    } else {
+        if (tail) hipLaunchKernelGGL((bwd_kernel<PRESET, MODE, DENSE, RAYS, CACHE, false, kCanTail>), grid, dim3(kBlock), shm, s, ka);
+        else hipLaunchKernelGGL((bwd_kernel<PRESET, MODE, DENSE, RAYS, CACHE, false>), grid, dim3(kBlock), shm, s, ka);
+    }
 }
 
 // the ray cache is used only by the culled, histogram-only variants (the training hot path)

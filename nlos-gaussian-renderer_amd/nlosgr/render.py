@@ -20,6 +20,10 @@ RAY_CACHE_MAX_BYTES = int(float(os.environ.get("NLOSGR_RAY_CACHE_GB", "128")) * 
 # the cache pays at small supports and costs at large ones (C3 backward, MI355X: 3 sigma 280 ms with the
 # cache vs 308 without; 5.7 sigma 1608 vs 1392 — the cached walk and the hand-off both slowed down)
 RAY_CACHE_MAX_CUTOFF = float(os.environ.get("NLOSGR_RAY_CACHE_MAX_CUTOFF", "4.5"))
+# occlusion engine row cache (the forward's per-ray (D, W) rows kept for the backward: 128 GiB at C3):
+# off by default, so the occlusion backward stays O(tile) in memory and re-runs the tile's forward
+# sweep instead; NLOSGR_OCCL_ROW_CACHE_GB > 0 allows it up to that size AND half the free device memory
+OCCL_ROW_CACHE_MAX_BYTES = int(float(os.environ.get("NLOSGR_OCCL_ROW_CACHE_GB", "0")) * 2 ** 30)
 
 
 @dataclass(frozen=True)
@@ -59,7 +63,11 @@ def use_ray_cache(cfg, geo, ng, want_rays=False):
     of every pair; for occlusion compositing the tiles' (D, W) rows, which spares the backward its
     re-run of the forward sweep."""
     if cfg.mode == "occl":
-        return bool(cfg.ray_cache) and not want_rays and tile_rows_bytes(geo) <= RAY_CACHE_MAX_BYTES
+        need = tile_rows_bytes(geo)
+        if not (bool(cfg.ray_cache) and not want_rays and 0 < need <= OCCL_ROW_CACHE_MAX_BYTES):
+            return False
+        free, _ = torch.cuda.mem_get_info(geo.wall.device)
+        return need <= free // 2
     return (bool(cfg.ray_cache) and 0 < cfg.cutoff <= RAY_CACHE_MAX_CUTOFF and not want_rays
             and cfg.mode in ("noocl", "netf") and cfg.selection == "support"
             and geo.nwall * ng * 24 <= RAY_CACHE_MAX_BYTES)

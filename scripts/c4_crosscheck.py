@@ -3,7 +3,11 @@ numerical point-sampled path on the C3 inputs (100k Gaussians -> 128x128x1024, c
 forward only, on one MI355X.  Prints one JSON line: relative L2 and max error per volume for each
 support cutoff, the stated tolerance, and the forward time of both paths.
 
-    python scripts/c4_crosscheck.py [--cutoffs 3,5] [--ng 100000] [--hw 128] [--t 1024]
+    python scripts/c4_crosscheck.py [--cutoffs 3,5] [--ng 100000] [--hw 128] [--t 1024] [--patha 64]
+
+Also times path A (the reference's analytic section renderer, nlosgr_rays_analytic + its per-ray
+3-sigma box filter: one value per ray, placed in the middle bin by section_renderer.py:163-184) on
+--patha evenly spaced wall points with their full 32x32 ray grids, extrapolated to the whole wall.
 
 Tolerance: the bin average differs from the point sample by ~ (dr^2 a / 24)(1 - a dr^2 kap^2)
 per ray segment, a = 1/sigma_r^2 along the ray, so per volume the relative L2 is
@@ -28,6 +32,7 @@ def main():
     ap.add_argument("--ng", type=int, default=100_000)
     ap.add_argument("--hw", type=int, default=128)
     ap.add_argument("--t", type=int, default=1024)
+    ap.add_argument("--patha", type=int, default=64)
     a = ap.parse_args()
     from nlosgr import GaussianParams
     from nlosgr.model import features_flat
@@ -60,7 +65,37 @@ def main():
         res.append({"cutoff": mc, "rel_l2": (d.norm() / h_n.norm()).item(),
                     "max_abs_err_over_max": (d.abs().max() / h_n.abs().max()).item(),
                     "fwd_ms_numerical": t_n, "fwd_ms_analytic": t_b})
-    out = {"config": f"C4: {a.ng} Gaussians -> {a.hw}x{a.hw}x{a.t}, 32x32 angular, cuda preset, no occlusion",
+    # path A: filter + analytic per wall point (rays of the geometry tables, t range (I1, I2) c dT)
+    from nlosgr.rays import filter_gaussians_per_ray, render_rays_analytic
+    from nlosgr.render import bboxes
+    P = a.hw * a.hw
+    sel = torch.linspace(0, P - 1, a.patha).round().long().tolist()
+    bb = bboxes(m._mu, m._scaling, m._rotation, 1.0, 3.0, preset="torch").view(-1, 6)
+    t0, t1 = float(geo_n.r[0]), float(geo_n.r[-1])
+    grids = []
+    for p in sel:
+        tg, pg = torch.meshgrid(geo_n.theta[p], geo_n.phi[p], indexing="ij")
+        tf, pf = tg.reshape(-1), pg.reshape(-1)
+        d = torch.stack([torch.sin(tf) * torch.cos(pf), torch.sin(tf) * torch.sin(pf), torch.cos(tf)], 1).contiguous()
+        cam = geo_n.wall[p].contiguous()
+        grids.append((cam.unsqueeze(0).expand(d.shape[0], 3).contiguous(), d, cam))
+
+    def path_a():
+        outs = []
+        for o, d, cam in grids:
+            filt = filter_gaussians_per_ray(o, d, m._mu, bb, 3.0)
+            outs.append(render_rays_analytic(o, d, t0, t1, filt, *params, cam, 3, 1.0, 1.28 / a.t, 1.0, 3.0))
+        return outs
+    path_a()
+    torch.cuda.synchronize()
+    ta = time.perf_counter()
+    vals = path_a()
+    torch.cuda.synchronize()
+    ms_a = (time.perf_counter() - ta) * 1e3
+    patha = {"wall_points_timed": len(sel), "ms_timed": ms_a, "ms_per_volume_extrapolated": ms_a * P / len(sel),
+             "max_ray_value": max(float(v.max()) for v in vals),
+             "note": "one value per ray (mid bin), not a transient: the reference path A's semantics"}
+    out = {"patha": patha, "config": f"C4: {a.ng} Gaussians -> {a.hw}x{a.hw}x{a.t}, 32x32 angular, cuda preset, no occlusion",
            "dr": dr, "s_min": s_min, "s_median": s_med,
            "tolerance_rel_l2": (dr / s_min) ** 2 / 24, "expected_rel_l2_median": (dr / s_med) ** 2 / 24,
            "results": res}

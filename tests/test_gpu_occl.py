@@ -207,3 +207,50 @@ def test_occl_row_cache_backward_equals_recompute(selection, cutoff):
     assert any(bool(x.abs().max() > 0) for x in d0)
     for a, b in zip(d0, d1):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("selection,cutoff", [("support", 5.7), ("support", 0.0), ("aabb", 0.0)])
+def test_occl_small_cdt_polynomial(selection, cutoff):
+    """c dT <= 1/64 (C3: 1.25e-3) takes the polynomial 1 - exp(-x) = x (1 - x/2 + x^2/6 - x^3/24)
+    (x = sigma pdf c dT <= c dT) in the forward rows and the backward pairs pass: same oracle
+    comparison as above at c dT = 0.015."""
+    from nlosgr.render import bboxes
+    walls, box = _scene()
+    m = _model(70, 2, 31, 1.2, 3.0)
+    g = torch.Generator().manual_seed(8)
+    gout = torch.randn(walls.shape[0], T, generator=g)
+    dt = 0.015
+    assert C * dt <= 1.0 / 64
+    hist, rays = _hip(m, "occl", selection, cutoff, walls, box, gout, want_rays=True, dt=dt)
+    bb = bboxes(m._mu, m._scaling, m._rotation, 1.0, 3.0, preset="cuda").reshape(-1, 6).cpu() \
+        if selection == "aabb" else None
+    P, ref, ref_rays = _oracle(m, True, walls, box, mc=cutoff if cutoff > 0 else None, bb=bb, gout=gout, dt=dt)
+    assert float(ref.abs().max()) > 0
+    _close(hist, ref, 2e-4, msg=f"occl small c dT hist {selection} {cutoff}")
+    _close(rays.reshape(ref_rays.shape), ref_rays, 2e-4, msg="occl small c dT rays")
+    _grads_close(m, P, 3e-4, f"occl small c dT {selection} {cutoff}")
+
+
+def test_aabb_early_exit_exact():
+    """AABB selection stops a tile's sweep once all its rays hold 256 selections: a scene where
+    every box covers every ray (the cap decides) renders identically with 600 Gaussians and with
+    the first 300 + 300 Gaussians that no ray can select any more (their indices come after every
+    ray's 256th hit)."""
+    from nlosgr import GaussianParams, features_flat
+    from nlosgr.geometry import build_geometry
+    from nlosgr.render import RenderConfig, render_forward, render_backward
+    walls, box = _scene()
+    m = _model(600, 1, 17, 2.5, 0.5)
+    geo = build_geometry(walls, box, NS, START, START + T, C, DELTAT, 0.5, "cuda", "occl")
+    cfg = RenderConfig(preset="cuda", mode="occl", sh_degree=1, cutoff=0.0, c_deltaT=C * DELTAT, selection="aabb")
+    full = (m._mu, m._scaling, m._rotation, m._opacity, features_flat(m).detach())
+    head = tuple(t[:300].contiguous() for t in full)
+    h_full, _ = render_forward(*full, geo, cfg)
+    h_head, _ = render_forward(*head, geo, cfg)
+    assert torch.equal(h_full, h_head)
+    gh = torch.randn_like(h_full)
+    d_full = render_backward(*full, geo, cfg, grad_hist=gh)
+    d_head = render_backward(*head, geo, cfg, grad_hist=gh)
+    for a, b in zip(d_full, d_head):
+        assert torch.equal(a[:300], b)
+        assert float(a[300:].abs().max()) == 0.0
