@@ -113,23 +113,26 @@ def cpu_baseline(cfg_name, cutoff, seed=0, preset="cuda", mode="noocl"):
                       f"points"}
 
 
-def committed_profile(cfg_name, kind, cutoff):
+def committed_profile(cfg_name, kind, cutoff, preset="cuda", mode="noocl", selection="support"):
     """The newest committed profiles/r*_<cfg>_<kind>.json (written by scripts/summarize_prof.py from
-    rocprofv3 passes of this bench command) recorded at the same cutoff, or (None, None)."""
+    rocprofv3 passes of this bench command) recorded for the same workload (cutoff, preset, mode,
+    selection; records without those keys are the default cuda / noocl / support workload), or
+    (None, None)."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{cfg_name.lower()}_{kind}.json")))
     for fn in reversed(files):
         with open(fn) as f:
             rec = json.load(f)
-        if rec.get("cutoff") == cutoff:
+        if (rec.get("cutoff") == cutoff and rec.get("preset", "cuda") == preset and rec.get("mode", "noocl") == mode
+                and rec.get("selection", "support") == selection):
             return rec, os.path.relpath(fn, ROOT)
     return None, None
 
 
-def pmc_traffic(cfg_name, kernels, cutoff):
+def pmc_traffic(cfg_name, kernels, cutoff, **wl):
     """HBM bytes per launch of `kernels` (name substrings): FETCH_SIZE x2 + WRITE_SIZE passes
-    (MI355X_MICROARCH.md §HBM), from the committed traffic profile, or None."""
-    rec, src = committed_profile(cfg_name, "traffic", cutoff)
+    (MI355X_MICROARCH.md §HBM), from the committed traffic profile of the same workload, or None."""
+    rec, src = committed_profile(cfg_name, "traffic", cutoff, **wl)
     if rec is None:
         return None, None
     total = 0.0
@@ -314,15 +317,18 @@ def main():
     pb = param_bytes(3)
     V = 4 * worst["nwall"] * T
     fwd_avg, bwd_avg = worst["fwd_ms"], worst["bwd_ms"]
+    tiles = a.mode == "occl" or a.selection == "aabb"     # ray-tile engine (csrc/nlosgr_tiles.hip)
     if bwd_avg >= fwd_avg:
         dom, dom_ms, dom_bytes = "bwd", bwd_avg, 2 * ng * pb + V
-        kern = ("preprocess_kernel", "bwd_kernel", "sh_kernel", "finish_kernel")
+        kern = (("preprocess_kernel", "tile_kernel", "tiles_finish_kernel") if tiles else
+                ("preprocess_kernel", "bwd_kernel", "sh_kernel", "finish_kernel"))
     else:
         dom, dom_ms, dom_bytes = "fwd", fwd_avg, ng * pb + V
-        kern = ("preprocess_kernel", "fwd_kernel")
+        kern = ("preprocess_kernel", "tile_kernel", "tiles_reduce_kernel") if tiles else ("preprocess_kernel", "fwd_kernel")
+    wl = {"preset": a.preset, "mode": a.mode, "selection": a.selection}
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
     single = a.band <= 1 and world == 1
-    traffic, traffic_src = pmc_traffic(a.config, kern, a.cutoff) if single else (None, None)
+    traffic, traffic_src = pmc_traffic(a.config, kern, a.cutoff, **wl) if single else (None, None)
     # compute-side figures: exact in-support evaluations of the (frozen) workload per second, and the
     # VALU issue utilisation from the committed SQ counter pass of this command
     # (SQ_INSTS_VALU x 2 cycles per wave64 instruction / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs); the 2
@@ -331,7 +337,7 @@ def main():
     valu = {"evaluations": ev, "pairs": worst["pairs"], "rays": worst["rays"],
             "evals_per_s_fwd": ev / (fwd_avg * 1e-3) if ev else None,
             "evals_per_s_bwd": ev / (bwd_avg * 1e-3) if (ev and bwd_avg) else None}
-    sq, sq_src = committed_profile(a.config, "valu", a.cutoff) if single else (None, None)
+    sq, sq_src = committed_profile(a.config, "valu", a.cutoff, **wl) if single else (None, None)
     if sq:
         valu["valu_issue_util"] = sq.get("valu_issue_util")
         valu["source"] = sq_src

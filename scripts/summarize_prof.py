@@ -50,6 +50,9 @@ def main(src, tag):
     bench = open(os.path.join(src, "bench_default.log")).read().strip().splitlines()[-1]
     line = json.loads(bench)
     cutoff = line["config"]["cutoff"]
+    # the workload the committed records belong to (bench.py matches on all four keys)
+    wl = {"cutoff": cutoff, "preset": line["config"].get("preset", "cuda"), "mode": line["config"].get("mode", "noocl"),
+          "selection": line["config"].get("selection", "support")}
     for f in glob.glob(os.path.join(src, "kt_*kernel_stats.csv")):
         shutil.copy(f, os.path.join(out, f"{tag}_kernel_stats.csv"))
     fetch = per_kernel(glob.glob(os.path.join(src, "fetch_*counter_collection.csv"))[0])
@@ -65,7 +68,7 @@ def main(src, tag):
                          "launches": max(len(fl), len(wl))}
     with open(os.path.join(out, f"{tag}_traffic.json"), "w") as f:
         json.dump({"source": f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE passes of bench.py ({tag})",
-                   "cutoff": cutoff, "kernels": res}, f, indent=1)
+                   **wl, "kernels": res}, f, indent=1)
     # the bench line read the previously committed traffic/VALU profiles when it ran: restate its
     # roofline.traffic from the passes of this same run
     kl = line["roofline"]["kernel"].split("(", 1)[1].rstrip(")").split(" + ")
@@ -89,11 +92,11 @@ def main(src, tag):
             avg["valu_issue_util"] = 2.0 * avg.get("SQ_INSTS_VALU", 0.0) / (128.0 * g) if g else None
             avg["launches"] = max(len(v) for v in c.values())
             kern[short(k)] = avg
-        dom = max((v for k, v in kern.items() if "fwd_kernel" in k or "bwd_kernel" in k),
+        dom = max((v for k, v in kern.items() if "fwd_kernel" in k or "bwd_kernel" in k or "tile_kernel" in k),
                   key=lambda v: v.get("GRBM_GUI_ACTIVE", 0.0), default=None)
         with open(os.path.join(out, f"{tag}_valu.json"), "w") as f:
             json.dump({"source": f"rocprofv3 --pmc SQ_* GRBM_GUI_ACTIVE pass of bench.py ({tag})",
-                       "cutoff": cutoff, "formula": "2 * SQ_INSTS_VALU / (128 * GRBM_GUI_ACTIVE)",
+                       **wl, "formula": "2 * SQ_INSTS_VALU / (128 * GRBM_GUI_ACTIVE)",
                        "valu_issue_util": dom["valu_issue_util"] if dom else None, "kernels": kern}, f, indent=1)
         with open(sqf[0]) as f, open(os.path.join(out, f"{tag}_sq_counters.csv"), "w", newline="") as g:
             rd = csv.DictReader(f)

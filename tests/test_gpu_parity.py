@@ -98,12 +98,20 @@ def test_volume_vs_oracle_sh_degree4(mode, cutoff):
     _volume_vs_oracle("torch", mode, cutoff, 4)
 
 
-def _volume_vs_oracle(preset, mode, cutoff, deg):
+@pytest.mark.parametrize("preset", ["torch", "cuda"])
+@pytest.mark.parametrize("cutoff", [0.0, 3.0, 5.7])
+def test_volume_vs_oracle_netf_small_cdt(preset, cutoff):
+    """netf at c dT <= 1/64 (T = 96: c dT = 0.0133; C3: 1.25e-3): the forward's transmittance factor
+    and the backward's a_j take the exp-free forms (om_exp_small, constant a_c) against the oracle."""
+    _volume_vs_oracle(preset, "netf", cutoff, 3, T=96)
+
+
+def _volume_vs_oracle(preset, mode, cutoff, deg, T=40):
     from nlosgr import GaussianParams, features_flat
     from nlosgr.geometry import build_geometry, relay_wall_grid, volume_box_point
     from nlosgr.render import RenderConfig, render
     dev = torch.device("cuda:0")
-    ng, ns, T = 48, 6, 40
+    ng, ns = 48, 6
     c, deltaT = 1.0, 1.28 / T
     start, end = T // 8, T // 8 + T
     model = GaussianParams.synthetic(ng, deg, preset=preset, device=dev, seed=3)
