@@ -72,6 +72,9 @@ struct KArgs {
     unsigned* cbox;              // ray cache [P][ng]: i0 | j0 << 12 | width << 24, 0 = not cached
     float* crho;                 // ray cache [P][ng]: the pair's SH albedo rho (1)
     int g_lo, g_hi;              // backward: Gaussians [g_lo, g_hi) (one bucket of the gradient all-reduce)
+    int pb0, pnw;                // backward: wall points [pb0, pb0 + pnw) of this launch (a batch; drho rows
+                                 // are indexed p - pb0, so the dL/drho buffer holds one batch, not the wall)
+    int accum;                   // backward batches after the first add into the partial slabs
 };
 
 // ray cache: a pair whose (theta, phi) candidate box has at most 128 cells records which cells
@@ -1019,7 +1022,7 @@ constexpr float kTailCutoff = 5.0f;
 template <int PRESET, int MODE, bool DENSE, bool RAYS, bool CACHE, bool SHR, bool TAIL = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) void bwd_kernel(KArgs k) {
     extern __shared__ __align__(16) float smem[];
-    const int nr = k.geo.nr, nt = k.geo.nt, np_ = k.geo.np, P_ = k.geo.nwall;
+    const int nr = k.geo.nr, nt = k.geo.nt, np_ = k.geo.np;
     constexpr bool shr = SHR;   // == (k.bshared != 0)
     const BwdLayout L(nr, nt, np_, shr);
     const int wave = threadIdx.x >> 6, lane = lane_id();
@@ -1036,8 +1039,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
     const int gi = gb + (shr ? wave * kNB : 0) + lane;
     const bool active = gi < k.g_hi;
     const int split = blockIdx.y;
-    const int per = (P_ + k.nsplit - 1) / k.nsplit;
-    const int pbeg = split * per, pend = min(P_, pbeg + per);
+    const int per = (k.pnw + k.nsplit - 1) / k.nsplit;
+    const int pbeg = k.pb0 + split * per, pend = min(k.pb0 + k.pnw, pbeg + per);
     const int deg = k.g.sh_degree;
     const int K = (deg + 1) * (deg + 1);
     const float mc2 = k.opt.cutoff * k.opt.cutoff;
@@ -1457,14 +1460,19 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
                 for (int cc = 0; cc < 3; ++cc) dA[3 * r + cc] += dU0p[r] * q[cc];
             for (int cc = 0; cc < 3; ++cc) dMu[cc] -= A[cc] * dU0p[0] + A[3 + cc] * dU0p[1] + A[6 + cc] * dU0p[2];
         }
-        if (active) k.drho[o] = (wpair > 0.f && !(k.opt.flags & 64)) ? drho_pair : 0.f;
+        if (active) k.drho[(size_t)(p - k.pb0) * k.g.ng + gio] = (wpair > 0.f && !(k.opt.flags & 64)) ? drho_pair : 0.f;
     }
     if (shr) {   // shared layout: every wave owns its Gaussians for the whole split
         if (active) {
+            // (rows of this split belong to this workgroup only; the first batch overwrites whatever the
+            // workspace held, later batches add)
             float* dst = k.partial + ((size_t)split * k.g.ng + gi) * 32;
-            for (int t = 0; t < 9; ++t) dst[t] = dA[t];
-            dst[9] = dMu[0]; dst[10] = dMu[1]; dst[11] = dMu[2];
-            dst[12] = dSig;
+            float v[kBwdSlots];
+            for (int t = 0; t < 9; ++t) v[t] = dA[t];
+            v[9] = dMu[0]; v[10] = dMu[1]; v[11] = dMu[2]; v[12] = dSig;
+            if (k.accum)
+                for (int t = 0; t < kBwdSlots; ++t) v[t] += dst[t];
+            for (int t = 0; t < kBwdSlots; ++t) dst[t] = v[t];
         }
         return;
     }
@@ -1483,7 +1491,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
         if (gb + g >= k.g_hi) continue;
         float s = 0.f;
         for (int w = 0; w < kWaves; ++w) s += red[(w * 64 + g) * kBwdSlots + c];
-        k.partial[((size_t)split * k.g.ng + gb + g) * 32 + c] = s;
+        float* dst = k.partial + ((size_t)split * k.g.ng + gb + g) * 32 + c;
+        *dst = k.accum ? *dst + s : s;
     }
 }
 
@@ -1499,9 +1508,8 @@ __global__ __launch_bounds__(kBlock) void sh_kernel(KArgs k) {
     const int gi = k.g_lo + blockIdx.x * blockDim.x + threadIdx.x;
     if (gi >= k.g_hi) return;
     const int split = blockIdx.y;
-    const int P_ = k.geo.nwall;
-    const int per = (P_ + k.nsh - 1) / k.nsh;
-    const int pbeg = split * per, pend = min(P_, pbeg + per);
+    const int per = (k.pnw + k.nsh - 1) / k.nsh;
+    const int pbeg = k.pb0 + split * per, pend = min(k.pb0 + k.pnw, pbeg + per);
     const int deg = k.g.sh_degree;
     const int K = (deg + 1) * (deg + 1);
     const GaussRec rec = k.recs[gi];
@@ -1512,7 +1520,7 @@ __global__ __launch_bounds__(kBlock) void sh_kernel(KArgs k) {
 #pragma unroll
     for (int c = 0; c < KM; ++c) dF[c] = 0.f;
     for (int p = pbeg; p < pend; ++p) {
-        const float drho = k.drho[(size_t)p * k.g.ng + gi];
+        const float drho = k.drho[(size_t)(p - k.pb0) * k.g.ng + gi];
         if (drho == 0.f) continue;
         const float q[3] = {k.geo.wall[3 * p] - mu[0], k.geo.wall[3 * p + 1] - mu[1], k.geo.wall[3 * p + 2] - mu[2]};
         float dir[3], nrm;
@@ -1529,9 +1537,15 @@ __global__ __launch_bounds__(kBlock) void sh_kernel(KArgs k) {
         dMu[0] += ox; dMu[1] += oy; dMu[2] += oz;
     }
     float* dst = k.shpart + ((size_t)split * k.g.ng + gi) * kShPart;
+    if (k.accum) {
 #pragma unroll
-    for (int c = 0; c < KM; ++c) dst[c] = dF[c];
-    dst[KM] = dMu[0]; dst[KM + 1] = dMu[1]; dst[KM + 2] = dMu[2];
+        for (int c = 0; c < KM; ++c) dst[c] += dF[c];
+        dst[KM] += dMu[0]; dst[KM + 1] += dMu[1]; dst[KM + 2] += dMu[2];
+    } else {
+#pragma unroll
+        for (int c = 0; c < KM; ++c) dst[c] = dF[c];
+        dst[KM] = dMu[0]; dst[KM + 1] = dMu[1]; dst[KM + 2] = dMu[2];
+    }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1639,7 +1653,28 @@ int bwd_nsplit(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlos
 
 // partial-slab splits the workspace layout reserves: the larger of the two layouts, so the ray
 // cache's offset does not depend on which layout a later backward picks (NLOSGR_BSHARED)
-int bwd_nsplit_ws(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_options* opt) {
+// The backward runs over batches of wall points so that its dL/drho buffer ([batch][ng], read by
+// sh_kernel) is bounded: NLOSGR_DRHO_MB (default 1024) MiB, i.e. C3 6.5 GB -> 1 GiB, a C5 rank 16.4 GB
+// -> 1 GiB.  Split counts are sized for one batch; batches after the first add into the partial slabs.
+int drho_batch(const nlosgr_gaussians* g, const nlosgr_geometry* geo) {
+    const char* e = getenv("NLOSGR_DRHO_MB");   // read per call (the workspace query and the launch agree)
+    const double mb = e ? atof(e) : 1024.0;
+    const long long budget = (long long)((mb > 0.0 ? mb : 1024.0) * 1048576.0);
+    const long long per = (long long)(g->ng > 0 ? g->ng : 1) * (long long)sizeof(float);
+    long long b = budget / per;
+    if (b < 1) b = 1;
+    if (b > geo->nwall) b = geo->nwall;
+    return (int)(b > 0 ? b : 1);
+}
+nlosgr_geometry batch_geo(const nlosgr_gaussians* g, const nlosgr_geometry* geo) {
+    nlosgr_geometry b = *geo;
+    b.nwall = drho_batch(g, geo);
+    return b;
+}
+
+int bwd_nsplit_ws(const nlosgr_gaussians* g, const nlosgr_geometry* geo0, const nlosgr_options* opt) {
+    const nlosgr_geometry gb = batch_geo(g, geo0);
+    const nlosgr_geometry* geo = &gb;
     const int a = bwd_nsplit(g, geo, opt, false), b = bwd_nsplit(g, geo, opt, true);
     return a > b ? a : b;
 }
@@ -1719,9 +1754,10 @@ size_t fpart_bytes(const nlosgr_gaussians* g, const nlosgr_geometry* geo) {
 }
 // after the ray cache: drho [P][ng] | sh partials [nsh][ng][kShPart] | 256-B diagnostics tail |
 // forward split partial histograms [nfsplit][P][nr]
-size_t sh_bytes(const nlosgr_gaussians* g, const nlosgr_geometry* geo) {
-    return align_up((size_t)geo->nwall * g->ng * sizeof(float)) +
-           align_up((size_t)sh_nsplit(g, geo) * g->ng * kShPart * sizeof(float));
+size_t sh_bytes(const nlosgr_gaussians* g, const nlosgr_geometry* geo0) {
+    const nlosgr_geometry gb = batch_geo(g, geo0);   // dL/drho for one wall-point batch
+    return align_up((size_t)gb.nwall * g->ng * sizeof(float)) +
+           align_up((size_t)sh_nsplit(g, &gb) * g->ng * kShPart * sizeof(float));
 }
 void cache_ptrs(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_options* opt, void* ws, int nsplit,
                 KArgs& ka) {
@@ -1874,14 +1910,15 @@ int nlosgr_render_bwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo, con
     ka.g_lo = opt->g_end > 0 ? opt->g_begin : 0;
     ka.g_hi = opt->g_end > 0 ? opt->g_end : g->ng;
     ka.bshared = bwd_shared(geo) ? 1 : 0;
-    ka.nsplit = bwd_nsplit(g, geo, opt, ka.bshared != 0);
+    const nlosgr_geometry gbat = batch_geo(g, geo);
+    ka.nsplit = bwd_nsplit(g, &gbat, opt, ka.bshared != 0);
     cache_ptrs(g, geo, opt, workspace, bwd_nsplit_ws(g, geo, opt), ka);
     {
         char* shb = (char*)workspace + align_up((size_t)g->ng * sizeof(GaussRec)) +
                     align_up((size_t)bwd_nsplit_ws(g, geo, opt) * g->ng * 32 * sizeof(float)) + cache_bytes(g, geo, opt);
         ka.drho = (float*)shb;
-        ka.shpart = (float*)(shb + align_up((size_t)geo->nwall * g->ng * sizeof(float)));
-        ka.nsh = sh_nsplit(g, geo);
+        ka.shpart = (float*)(shb + align_up((size_t)gbat.nwall * g->ng * sizeof(float)));   // drho: one batch
+        ka.nsh = sh_nsplit(g, &gbat);
         if (opt->flags & 8) {   // diagnostics: counters in the workspace's 256-B tail
             ka.counts = (unsigned long long*)(shb + sh_bytes(g, geo));
             HIPCHK(hipMemsetAsync(ka.counts, 0, 8 * sizeof(unsigned long long), s));
@@ -1893,22 +1930,27 @@ int nlosgr_render_bwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo, con
         const size_t shm = (size_t)BwdLayout(geo->nr, geo->nt, geo->np, ka.bshared != 0).total * sizeof(float);
         const bool dense = !(opt->cutoff > 0.f);
         const bool rays = grad_ray != nullptr;
-        if (g->preset == NLOSGR_PRESET_TORCH) {
-            if (opt->mode == NLOSGR_MODE_NOOCL) dispatch_bwd<0, 0>(ka, dense, rays, shm, s);
-            else dispatch_bwd<0, 1>(ka, dense, rays, shm, s);
-        } else {
-            if (opt->mode == NLOSGR_MODE_NOOCL) dispatch_bwd<1, 0>(ka, dense, rays, shm, s);
-            else dispatch_bwd<1, 1>(ka, dense, rays, shm, s);
-        }
-        HIPCHK(hipGetLastError());
         const dim3 shgrid((ka.g_hi - ka.g_lo + kBlock - 1) / kBlock, ka.nsh);
-        if (g->preset == NLOSGR_PRESET_TORCH && g->sh_degree == 4)
-            hipLaunchKernelGGL((sh_kernel<NLOSGR_PRESET_TORCH, kMaxK4>), shgrid, dim3(kBlock), 0, s, ka);
-        else if (g->preset == NLOSGR_PRESET_TORCH)
-            hipLaunchKernelGGL((sh_kernel<NLOSGR_PRESET_TORCH, kMaxK>), shgrid, dim3(kBlock), 0, s, ka);
-        else
-            hipLaunchKernelGGL((sh_kernel<NLOSGR_PRESET_CUDA, kMaxK>), shgrid, dim3(kBlock), 0, s, ka);
-        HIPCHK(hipGetLastError());
+        for (int pb0 = 0; pb0 < geo->nwall; pb0 += gbat.nwall) {   // wall-point batches (drho_batch)
+            ka.pb0 = pb0;
+            ka.pnw = geo->nwall - pb0 < gbat.nwall ? geo->nwall - pb0 : gbat.nwall;
+            ka.accum = pb0 > 0 ? 1 : 0;
+            if (g->preset == NLOSGR_PRESET_TORCH) {
+                if (opt->mode == NLOSGR_MODE_NOOCL) dispatch_bwd<0, 0>(ka, dense, rays, shm, s);
+                else dispatch_bwd<0, 1>(ka, dense, rays, shm, s);
+            } else {
+                if (opt->mode == NLOSGR_MODE_NOOCL) dispatch_bwd<1, 0>(ka, dense, rays, shm, s);
+                else dispatch_bwd<1, 1>(ka, dense, rays, shm, s);
+            }
+            HIPCHK(hipGetLastError());
+            if (g->preset == NLOSGR_PRESET_TORCH && g->sh_degree == 4)
+                hipLaunchKernelGGL((sh_kernel<NLOSGR_PRESET_TORCH, kMaxK4>), shgrid, dim3(kBlock), 0, s, ka);
+            else if (g->preset == NLOSGR_PRESET_TORCH)
+                hipLaunchKernelGGL((sh_kernel<NLOSGR_PRESET_TORCH, kMaxK>), shgrid, dim3(kBlock), 0, s, ka);
+            else
+                hipLaunchKernelGGL((sh_kernel<NLOSGR_PRESET_CUDA, kMaxK>), shgrid, dim3(kBlock), 0, s, ka);
+            HIPCHK(hipGetLastError());
+        }
     } else {
         HIPCHK(hipMemsetAsync(ka.partial, 0, (size_t)ka.nsplit * g->ng * 32 * sizeof(float), s));
         ka.nsh = 0;

@@ -325,3 +325,22 @@ def test_rccl_exchange_single_rank():
     for a, b, c in zip(ref, got, bucketed):
         assert torch.equal(a, b) and torch.equal(a, c)
     torch.testing.assert_close(loss2, torch.tensor([0.5, 2.0]))
+
+
+def test_backward_wall_batches_equal_single_batch(monkeypatch):
+    """The backward's wall-point batches (bounded dL/drho buffer, NLOSGR_DRHO_MB) give the gradients of
+    a single batch: 3 batches vs 1 (summation order of the batch partials differs: rel 1e-5)."""
+    from nlosgr import features_flat
+    from nlosgr.render import render_backward, render_forward
+    dev = torch.device("cuda:0")
+    scene, model, geo, cfg, target = _scene_model(dev, ng=1500)
+    args = (model._mu.detach(), model._scaling.detach(), model._rotation.detach(), model._opacity.detach(),
+            features_flat(model).detach().contiguous())
+    hist, _ = render_forward(*args, geo, cfg)
+    grad = torch.randn_like(hist)
+    ref = render_backward(*args, geo, cfg, grad_hist=grad)
+    # 1500 Gaussians x 4 B x 11 wall points per batch: 30 wall points -> 3 batches
+    monkeypatch.setenv("NLOSGR_DRHO_MB", str(1500 * 4 * 11 / 1048576.0))
+    got = render_backward(*args, geo, cfg, grad_hist=grad)
+    for a, b in zip(got, ref):
+        assert _rel(a, b) <= 1e-5
