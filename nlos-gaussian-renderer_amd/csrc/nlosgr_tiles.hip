@@ -7,7 +7,8 @@
 //       T_k = exp(-c dT sum_{k'<k} D_k'),  out_k = T_k W_k, and 0 from the first T_k < 1e-4 on;
 //   * NLOSGR_SELECT_AABB — path C's filter (ray_aabb.cu:10-61 + volume_renderer.cu:220-245): a ray
 //       sums only the first 256 Gaussians, by index, whose 3-sigma box (bbox_compute.cuh) it hits,
-//       each over the whole ray (bins with m^2 <= kFullM2; beyond, pdf < 1e-39 underflows anyway).
+//       each over the whole ray (cutoff <= 0: bins with m^2 <= kFullM2; beyond, pdf < 1e-39 underflows
+//       anyway) or over its bins within the Mahalanobis cutoff (5.7: terms < 9e-8 of its peak dropped).
 // With NLOSGR_SELECT_SUPPORT a ray sums every Gaussian over the bins within the Mahalanobis cutoff
 // (dense when cutoff <= 0), as the pair-major kernels do.
 //
@@ -224,7 +225,10 @@ __global__ __launch_bounds__(tile_threads<BWD>()) void tile_kernel(TArgs k) {
     float* cone = misc + 144;                           // axis xyz, cos h, sin h, pass-all flag
     const int tid = threadIdx.x, wave = tid >> 6, lane = lane_id();
     const int RT = k.rt;
-    const float mc2 = SEL == NLOSGR_SELECT_AABB ? kFullM2 : k.opt.cutoff * k.opt.cutoff;
+    // AABB selection: each selected Gaussian over the samples within the cutoff (5.7 sigma = parity
+    // grade: terms below 9e-8 of its peak dropped), or the whole representable ray (cutoff <= 0)
+    const float mc2 = SEL == NLOSGR_SELECT_AABB ? (k.opt.cutoff > 0.f ? k.opt.cutoff * k.opt.cutoff : kFullM2)
+                                                : k.opt.cutoff * k.opt.cutoff;
     const float r0 = k.geo.r[0];
     const float dr = nr > 1 ? (k.geo.r[nr - 1] - r0) / (float)(nr - 1) : 1.0f;
     const float inv_dr = 1.0f / dr;

@@ -126,8 +126,11 @@ def test_occl_early_termination():
 
 @pytest.mark.parametrize("occl", [False, True])
 @pytest.mark.parametrize("ng,shift", [(50, 1.2), (300, 2.5)])
-def test_aabb_selection_vs_oracle(occl, ng, shift):
-    """Path C's own selection: 3-sigma boxes, first 256 hits per ray by index, whole-ray pdf.
+@pytest.mark.parametrize("cutoff", [0.0, 5.7])
+def test_aabb_selection_vs_oracle(occl, ng, shift, cutoff):
+    """Path C's own selection: 3-sigma boxes, first 256 hits per ray by index, whole-ray pdf (the
+    oracle); the engine evaluates each selected Gaussian over the whole ray (cutoff 0) or over its
+    5.7-sigma samples (terms < 9e-8 of its peak dropped: the same tolerances hold).
     (300, 2.5): every box covers every ray, so the 256 cap decides which Gaussians a ray sees."""
     from nlosgr.render import bboxes
     walls, box = _scene()
@@ -135,7 +138,7 @@ def test_aabb_selection_vs_oracle(occl, ng, shift):
     g = torch.Generator().manual_seed(6)
     gout = torch.randn(walls.shape[0], T, generator=g)
     mode = "occl" if occl else "noocl"
-    hist, rays = _hip(m, mode, "aabb", 0.0, walls, box, gout, want_rays=True)
+    hist, rays = _hip(m, mode, "aabb", cutoff, walls, box, gout, want_rays=True)
     bb = bboxes(m._mu, m._scaling, m._rotation, 1.0, 3.0, preset="cuda").reshape(-1, 6).cpu()
     P, ref, ref_rays = _oracle(m, occl, walls, box, bb=bb, gout=gout)
     if ng == 300:
