@@ -137,7 +137,7 @@ def pmc_traffic(cfg_name, kernels, cutoff, **wl):
         return None, None
     total = 0.0
     for sub in kernels:
-        hits = [v["hbm_bytes_per_launch"] for k, v in rec["kernels"].items() if sub in k]
+        hits = [v.get("hbm_bytes_per_step", v["hbm_bytes_per_launch"]) for k, v in rec["kernels"].items() if sub in k]
         if not hits:
             return None, None
         total += max(hits)

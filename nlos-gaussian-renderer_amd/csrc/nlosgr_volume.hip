@@ -436,7 +436,14 @@ __device__ __forceinline__ void enumerate_cached(unsigned long long& bits0, unsi
 
 __device__ __forceinline__ void compiler_fence() { __asm__ __volatile__("" ::: "memory"); }
 
-template <int PRESET, int MODE, bool DENSE, bool RAYS, bool CACHE>
+// TAIL (culled no-occlusion histogram at cutoff >= kTailCutoff): the forward drain adds no masks.  A
+// round starts the recurrence at the even bin at or below pos and adds all kSteps values: the bins
+// before pos (one, o = 1) and past the segment's end (up to kSteps - 1) get their exact Gaussian
+// values, each < exp(-m_c^2 / 2) of the Gaussian's peak (<= 3.7e-6 at m_c >= kTailCutoff), so the
+// result lies between the culled and the dense sum.  Bins past nr land in the zeroed pad row.
+constexpr float kTailCutoff = 5.0f;
+
+template <int PRESET, int MODE, bool DENSE, bool RAYS, bool CACHE, bool TAIL = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) void fwd_kernel(KArgs k) {
     extern __shared__ __align__(16) float smem[];
     const int nr = k.geo.nr, nt = k.geo.nt, np_ = k.geo.np;
@@ -579,7 +586,26 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
                 // per-step mask switching).
                 const int o = d.pos & (VW - 1);
                 const int lim = remw + o;   // slot j is in the segment iff o <= j < lim
-                if (win) {
+                if (TAIL && win) {
+                    const float t0 = t - (float)o;   // slot 0 = the even bin at or below pos
+                    float cur = fast_exp2(fmaf(d.ga, t0 * t0, d.al));
+                    float q = fast_exp2(d.ga * fmaf(2.f, t0, 1.f));
+                    const float cc = fast_exp2(2.f * d.ga);
+                    float2* hb2 = reinterpret_cast<float2*>(hb);
+#pragma unroll
+                    for (int kv = 0; kv < kSteps / VW; ++kv) {
+                        const float v0 = cur;
+                        cur *= q;
+                        q *= cc;
+                        const float v1 = cur;
+                        cur *= q;
+                        q *= cc;
+                        float2 x = hb2[kv];
+                        x.x += v0; x.y += v1;
+                        hb2[kv] = x;
+                        compiler_fence();
+                    }
+                } else if (win) {
                     float cur = fast_exp2(fmaf(d.ga, t * t, d.al));
                     float q = fast_exp2(d.ga * fmaf(2.f, t, 1.f));
                     const float cc = fast_exp2(2.f * d.ga);
@@ -1017,9 +1043,10 @@ __device__ __forceinline__ bool bray_setup(const float* pd, float2 th, float2 ph
 
 // TAIL (culled no-occlusion histogram backward at cutoff >= kTailCutoff): the drain reads the upstream
 // row without the segment-end mask, see BV below
-constexpr float kTailCutoff = 5.0f;
 
-template <int PRESET, int MODE, bool DENSE, bool RAYS, bool CACHE, bool SHR, bool TAIL = false>
+// NBLK: a lane whose finished result waits for its hand-off still takes a new ray (the result's pair
+// slot and ray cell move to pslot / pij); it blocks only when that ray ends before the hand-off
+template <int PRESET, int MODE, bool DENSE, bool RAYS, bool CACHE, bool SHR, bool TAIL = false, bool NBLK = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) void bwd_kernel(KArgs k) {
     extern __shared__ __align__(16) float smem[];
     const int nr = k.geo.nr, nt = k.geo.nt, np_ = k.geo.np;
@@ -1159,6 +1186,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
         b.S0b = b.S1b = b.S2b = b.dsigb = 0.f;
         // pending result of a finished ray: dL/du0, dL/dv, dsigma, drho
         float rU[3] = {0.f, 0.f, 0.f}, rV[3] = {0.f, 0.f, 0.f}, rSig = 0.f, rRho = 0.f;
+        int pslot = lane, pij = 0;   // pair slot and ray cell of the pending result
         while (true) {
             if (CACHE && qcount < 64 && __builtin_amdgcn_ballot_w64((cbits0 | cbits1) != 0ull)) {
                 wave_sync();
@@ -1172,11 +1200,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
             }
             const bool anymore = __builtin_amdgcn_ballot_w64(more || (CACHE && (cbits0 | cbits1) != 0ull)) != 0;
             // a lane whose finished result still waits for its hand-off takes no new ray
-            const unsigned long long idle = __builtin_amdgcn_ballot_w64(!act && !pend);
+            const unsigned long long idle = __builtin_amdgcn_ballot_w64(!act && (NBLK || !pend));
             const int nidle = __popcll(idle);
             if (qcount > 0 && (nidle >= kBRefill || !anymore)) {
                 const int r = lanes_below(idle);
-                const bool take = !act && !pend && r < qcount;
+                const bool take = !act && (NBLK || !pend) && r < qcount;
                 if (take && !(k.opt.flags & 1)) {                  // flags 1: enumerate only
                     const unsigned e = rayq[(qhead + r) & (kRQ - 1)];
                     const int slot = e & 0xFF, i = (e >> 8) & 0xFFF, j = e >> 20;
@@ -1402,6 +1430,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
                             rU[r] = -zv;
                             rV[r] = -(b.ts * zv + S1 * b.zs[r] + S2 * b.v[r]);
                         }
+                        pslot = b.slot;
+                        pij = b.ij;
                         act = false;
                         pend = !(k.opt.flags & 32);   // flags 32 (diagnostics): drop results, no hand-off
                     }
@@ -1412,12 +1442,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
                 // hand finished rays to their pair lanes: per pair and round one claimant (stamped
                 // claim in LDS), its result fetched by the pair lane with bpermute
                 const unsigned stamp = (round << 8) | (unsigned)lane;
-                if (pend) owner[b.slot] = stamp;
+                if (pend) owner[pslot] = stamp;
                 wave_sync();
                 const unsigned ow = owner[lane];
                 const bool got = (ow >> 8) == (round & 0xFFFFFFu);
                 const int src = got ? (int)(ow & 63u) : lane;
-                const bool won = pend && owner[b.slot] == stamp;
+                const bool won = pend && owner[pslot] == stamp;
                 const float gm = got ? 1.f : 0.f;
                 float gU[3], gV[3];
                 // every lane must execute the bpermute: it cannot read lanes that are inactive in EXEC
@@ -1425,7 +1455,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
                 for (int c = 0; c < 3; ++c) { gU[c] = gm * __shfl(rU[c], src); gV[c] = gm * __shfl(rV[c], src); }
                 const float gSig = gm * __shfl(rSig, src);
                 const float gRho = MODE == NLOSGR_MODE_NOOCL ? 0.f : gm * __shfl(rRho, src);
-                const int sij = __shfl(b.ij, src);
+                const int sij = __shfl(pij, src);
                 const int gij = got ? sij : 0;
                 const float2 th = tth[gij & 0xFFFF], ph = tph[gij >> 16];
                 const float d3[3] = {th.x * ph.x, th.x * ph.y, th.y};
@@ -1682,8 +1712,13 @@ int bwd_nsplit_ws(const nlosgr_gaussians* g, const nlosgr_geometry* geo0, const 
 
 template <int PRESET, int MODE, bool DENSE, bool RAYS, bool CACHE>
 void launch_fwd(const KArgs& ka, size_t shm, hipStream_t s) {
-    hipLaunchKernelGGL((fwd_kernel<PRESET, MODE, DENSE, RAYS, CACHE>), dim3(ka.geo.nwall, ka.hpart ? ka.nfsplit : 1),
-                       dim3(kBlock), shm, s, ka);
+    const dim3 grid(ka.geo.nwall, ka.hpart ? ka.nfsplit : 1);
+    constexpr bool kCanTail = MODE == NLOSGR_MODE_NOOCL && !DENSE && !RAYS;
+    // NLOSGR_FTAIL=0: masked forward drain at every cutoff (A/B and parity cross-check)
+    const char* ftail = getenv("NLOSGR_FTAIL");
+    const bool tail = kCanTail && ka.opt.cutoff >= kTailCutoff && !ka.counts && !(ftail && ftail[0] == '0');
+    if (tail) hipLaunchKernelGGL((fwd_kernel<PRESET, MODE, DENSE, RAYS, CACHE, kCanTail>), grid, dim3(kBlock), shm, s, ka);
+    else hipLaunchKernelGGL((fwd_kernel<PRESET, MODE, DENSE, RAYS, CACHE>), grid, dim3(kBlock), shm, s, ka);
 }
 template <int PRESET, int MODE, bool DENSE, bool RAYS, bool CACHE>
 void launch_bwd(const KArgs& ka, size_t shm, hipStream_t s) {
@@ -1691,6 +1726,11 @@ void launch_bwd(const KArgs& ka, size_t shm, hipStream_t s) {
     dim3 grid((ka.g_hi - ka.g_lo + gpb - 1) / gpb, ka.nsplit);
     constexpr bool kCanTail = MODE == NLOSGR_MODE_NOOCL && !DENSE && !RAYS;
     const bool tail = kCanTail && ka.opt.cutoff >= kTailCutoff;
+    const char* nb = getenv("NLOSGR_BNBLK");   // A/B: non-blocking hand-off (NBLK)
+    if (tail && !ka.bshared && nb && nb[0] == '1') {
+        hipLaunchKernelGGL((bwd_kernel<PRESET, MODE, DENSE, RAYS, CACHE, false, kCanTail, true>), grid, dim3(kBlock), shm, s, ka);
+        return;
+    }
     if (ka.bshared) {
         if (tail) hipLaunchKernelGGL((bwd_kernel<PRESET, MODE, DENSE, RAYS, CACHE, true, kCanTail>), grid, dim3(kBlock), shm, s, ka);
         else hipLaunchKernelGGL((bwd_kernel<PRESET, MODE, DENSE, RAYS, CACHE, true>), grid, dim3(kBlock), shm, s, ka);

@@ -1,0 +1,78 @@
+"""Same-process A/B of run-time switches (env vars the library reads per call) on one config:
+forward and backward of the no-occlusion volume, variants interleaved, median of --reps.
+
+    python scripts/ab_env.py [--config C3] [--cutoff 5.7] [--reps 3] [--bwd] VAR=a,VAR2=b  VAR=c ...
+
+Each positional argument is one variant (comma-separated NAME=VALUE pairs, '-' for none).  Prints one
+JSON line: per variant fwd/bwd medians and the forward's rel-L2 against the first variant."""
+import argparse, dataclasses, json, os, statistics, sys, time
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, 'nlos-gaussian-renderer_amd')); sys.path.insert(0, ROOT)
+import torch
+from nlosgr import GaussianParams, features_flat
+from nlosgr.volume import Scene, make_config
+from nlosgr.render import render_backward, render_forward
+
+ap = argparse.ArgumentParser()
+ap.add_argument('--config', default='C3')
+ap.add_argument('--cutoff', type=float, default=5.7)
+ap.add_argument('--reps', type=int, default=3)
+ap.add_argument('--bwd', action='store_true')
+ap.add_argument('--mode', default='noocl')
+ap.add_argument('variants', nargs='+')
+a = ap.parse_args()
+ng, H, T = {'C3': (100_000, 128, 1024), 'S1': (20_000, 32, 512), 'C2': (50_000, 64, 512)}[a.config]
+dev = torch.device('cuda:0')
+scene = Scene(H=H, W=H, T=T, ns=32)
+m = GaussianParams.synthetic(ng, 3, preset='cuda', device=dev, seed=0)
+geo = scene.geometry(dev, 'cuda', a.mode)
+args = (m._mu.detach(), m._scaling.detach(), m._rotation.detach(), m._opacity.detach(), features_flat(m).detach(), geo)
+cfg = dataclasses.replace(make_config(m, scene, 'cuda', cutoff=a.cutoff), mode=a.mode)
+
+
+def setenv(v):
+    for kv in v.split(','):
+        if kv and kv != '-':
+            k, val = kv.split('=', 1)
+            os.environ[k] = val
+
+
+def unsetenv(v):
+    for kv in v.split(','):
+        if kv and kv != '-':
+            os.environ.pop(kv.split('=', 1)[0], None)
+
+
+grad = None
+res = {v: {'fwd': [], 'bwd': []} for v in a.variants}
+out = {}
+for rep in range(a.reps + 1):
+    for v in a.variants:
+        setenv(v)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        hist, _ = render_forward(*args, cfg)
+        torch.cuda.synchronize()
+        tf = (time.perf_counter() - t0) * 1e3
+        if grad is None:
+            grad = torch.randn_like(hist) * 1e-3
+        tb = 0.0
+        if a.bwd:
+            t0 = time.perf_counter()
+            render_backward(*args, cfg, grad_hist=grad)
+            torch.cuda.synchronize()
+            tb = (time.perf_counter() - t0) * 1e3
+        unsetenv(v)
+        if rep == 0:
+            out[v] = hist
+            continue
+        res[v]['fwd'].append(tf)
+        res[v]['bwd'].append(tb)
+        print(f'rep {rep} {v}: fwd {tf:.1f} bwd {tb:.1f} ms', file=sys.stderr, flush=True)
+ref = out[a.variants[0]]
+line = {'config': a.config, 'cutoff': a.cutoff, 'mode': a.mode, 'variants': {}}
+for v in a.variants:
+    med = lambda x: statistics.median(x) if x else None
+    line['variants'][v] = {'fwd_ms': med(res[v]['fwd']), 'bwd_ms': med(res[v]['bwd']),
+                           'rel_l2_vs_first': ((out[v] - ref).norm() / ref.norm()).item()}
+print(json.dumps(line))

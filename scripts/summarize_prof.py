@@ -53,6 +53,7 @@ def main(src, tag):
     # the workload the committed records belong to (bench.py matches on all four keys)
     wl = {"cutoff": cutoff, "preset": line["config"].get("preset", "cuda"), "mode": line["config"].get("mode", "noocl"),
           "selection": line["config"].get("selection", "support")}
+    nsteps = line["steps"] + line["warmup"]
     for f in glob.glob(os.path.join(src, "kt_*kernel_stats.csv")):
         shutil.copy(f, os.path.join(out, f"{tag}_kernel_stats.csv"))
     fetch = per_kernel(glob.glob(os.path.join(src, "fetch_*counter_collection.csv"))[0])
@@ -61,18 +62,20 @@ def main(src, tag):
     for k in sorted(set(fetch) | set(write)):
         if not ours(k):
             continue
-        fl, wl = fetch.get(k, {}).get("FETCH_SIZE", []), write.get(k, {}).get("WRITE_SIZE", [])
+        fl, wr_ = fetch.get(k, {}).get("FETCH_SIZE", []), write.get(k, {}).get("WRITE_SIZE", [])
         fb = 2.0 * 1024 * sum(fl) / max(1, len(fl))
-        wb = 1024 * sum(wl) / max(1, len(wl))
+        wb = 1024 * sum(wr_) / max(1, len(wr_))
+        n = max(len(fl), len(wr_))
+        # per step: the backward runs one bwd_kernel / sh_kernel launch per wall-point batch
         res[short(k)] = {"fetch_bytes_x2": fb, "write_bytes": wb, "hbm_bytes_per_launch": fb + wb,
-                         "launches": max(len(fl), len(wl))}
+                         "launches": n, "launches_per_step": n / nsteps, "hbm_bytes_per_step": (fb + wb) * n / nsteps}
     with open(os.path.join(out, f"{tag}_traffic.json"), "w") as f:
         json.dump({"source": f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE passes of bench.py ({tag})",
                    **wl, "kernels": res}, f, indent=1)
     # the bench line read the previously committed traffic/VALU profiles when it ran: restate its
     # roofline.traffic from the passes of this same run
     kl = line["roofline"]["kernel"].split("(", 1)[1].rstrip(")").split(" + ")
-    hits = [[v["hbm_bytes_per_launch"] for k, v in res.items() if sub in k] for sub in kl]
+    hits = [[v["hbm_bytes_per_step"] for k, v in res.items() if sub in k] for sub in kl]
     if all(hits):
         line["roofline"]["traffic"] = sum(max(h) for h in hits)
         line["roofline"]["traffic_source"] = f"profiles/{tag}_traffic.json"
@@ -93,7 +96,7 @@ def main(src, tag):
             avg["launches"] = max(len(v) for v in c.values())
             kern[short(k)] = avg
         dom = max((v for k, v in kern.items() if "fwd_kernel" in k or "bwd_kernel" in k or "tile_kernel" in k),
-                  key=lambda v: v.get("GRBM_GUI_ACTIVE", 0.0), default=None)
+                  key=lambda v: v.get("GRBM_GUI_ACTIVE", 0.0) * v["launches"], default=None)   # busiest over the run
         with open(os.path.join(out, f"{tag}_valu.json"), "w") as f:
             json.dump({"source": f"rocprofv3 --pmc SQ_* GRBM_GUI_ACTIVE pass of bench.py ({tag})",
                        **wl, "formula": "2 * SQ_INSTS_VALU / (128 * GRBM_GUI_ACTIVE)",
@@ -111,7 +114,7 @@ def main(src, tag):
     with open(os.path.join(out, f"{tag}_bench.json"), "w") as f:
         f.write(json.dumps(line) + "\n")
     for k, v in res.items():
-        print(f"{v['hbm_bytes_per_launch'] / 1e6:10.2f} MB  {k[:90]}")
+        print(f"{v['hbm_bytes_per_step'] / 1e6:10.2f} MB/step ({v['launches_per_step']:.2f} launches)  {k[:90]}")
 
 
 if __name__ == "__main__":

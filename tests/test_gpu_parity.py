@@ -156,7 +156,9 @@ def test_cutoff_converges_to_dense():
     # 6 sigma sits at the fp32 summation-order floor (dense and culled sum in different orders;
     # 2.0e-6 / 2.3e-6 for two candidate-box rules that enumerate identical rays and samples)
     assert errs[0] < 5e-2 and errs[1] < 3e-3 and errs[2] < 1e-4 and errs[3] < 4e-6, errs
-    assert all(errs[i + 1] <= errs[i] for i in range(3)), errs
+    # monotone down to that floor (at cutoff >= 5 the drains also add the Gaussian tails of a segment's
+    # last round, so 5 sigma can reach the floor as well)
+    assert all(errs[i + 1] <= errs[i] or errs[i + 1] < 4e-6 for i in range(3)), errs
 
 
 @pytest.mark.parametrize("preset", ["torch", "cuda"])
