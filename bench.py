@@ -343,7 +343,7 @@ def main():
         valu["source"] = sq_src
     out = {
         "metric": "transient volumes/sec (fwd+bwd), 100k Gaussians → 128×128×1024 ToF bins"
-        if a.config == "C3" and (a.preset, a.mode) == ("cuda", "noocl")
+        if a.config == "C3" and (a.preset, a.mode, a.selection) == ("cuda", "noocl", "support")
         else f"transient volumes/sec ({'fwd' if fwd_only else 'fwd+bwd'}) {a.config}",
         "value": volumes_per_s, "unit": "volumes/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
         "ms_per_step": ms_per_step, "higher_is_better": True,

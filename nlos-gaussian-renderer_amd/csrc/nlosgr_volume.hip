@@ -1044,9 +1044,7 @@ __device__ __forceinline__ bool bray_setup(const float* pd, float2 th, float2 ph
 // TAIL (culled no-occlusion histogram backward at cutoff >= kTailCutoff): the drain reads the upstream
 // row without the segment-end mask, see BV below
 
-// NBLK: a lane whose finished result waits for its hand-off still takes a new ray (the result's pair
-// slot and ray cell move to pslot / pij); it blocks only when that ray ends before the hand-off
-template <int PRESET, int MODE, bool DENSE, bool RAYS, bool CACHE, bool SHR, bool TAIL = false, bool NBLK = false>
+template <int PRESET, int MODE, bool DENSE, bool RAYS, bool CACHE, bool SHR, bool TAIL = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) void bwd_kernel(KArgs k) {
     extern __shared__ __align__(16) float smem[];
     const int nr = k.geo.nr, nt = k.geo.nt, np_ = k.geo.np;
@@ -1186,7 +1184,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
         b.S0b = b.S1b = b.S2b = b.dsigb = 0.f;
         // pending result of a finished ray: dL/du0, dL/dv, dsigma, drho
         float rU[3] = {0.f, 0.f, 0.f}, rV[3] = {0.f, 0.f, 0.f}, rSig = 0.f, rRho = 0.f;
-        int pslot = lane, pij = 0;   // pair slot and ray cell of the pending result
         while (true) {
             if (CACHE && qcount < 64 && __builtin_amdgcn_ballot_w64((cbits0 | cbits1) != 0ull)) {
                 wave_sync();
@@ -1200,11 +1197,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
             }
             const bool anymore = __builtin_amdgcn_ballot_w64(more || (CACHE && (cbits0 | cbits1) != 0ull)) != 0;
             // a lane whose finished result still waits for its hand-off takes no new ray
-            const unsigned long long idle = __builtin_amdgcn_ballot_w64(!act && (NBLK || !pend));
+            const unsigned long long idle = __builtin_amdgcn_ballot_w64(!act && !pend);
             const int nidle = __popcll(idle);
             if (qcount > 0 && (nidle >= kBRefill || !anymore)) {
                 const int r = lanes_below(idle);
-                const bool take = !act && (NBLK || !pend) && r < qcount;
+                const bool take = !act && !pend && r < qcount;
                 if (take && !(k.opt.flags & 1)) {                  // flags 1: enumerate only
                     const unsigned e = rayq[(qhead + r) & (kRQ - 1)];
                     const int slot = e & 0xFF, i = (e >> 8) & 0xFFF, j = e >> 20;
@@ -1430,8 +1427,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
                             rU[r] = -zv;
                             rV[r] = -(b.ts * zv + S1 * b.zs[r] + S2 * b.v[r]);
                         }
-                        pslot = b.slot;
-                        pij = b.ij;
                         act = false;
                         pend = !(k.opt.flags & 32);   // flags 32 (diagnostics): drop results, no hand-off
                     }
@@ -1442,12 +1437,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
                 // hand finished rays to their pair lanes: per pair and round one claimant (stamped
                 // claim in LDS), its result fetched by the pair lane with bpermute
                 const unsigned stamp = (round << 8) | (unsigned)lane;
-                if (pend) owner[pslot] = stamp;
+                if (pend) owner[b.slot] = stamp;
                 wave_sync();
                 const unsigned ow = owner[lane];
                 const bool got = (ow >> 8) == (round & 0xFFFFFFu);
                 const int src = got ? (int)(ow & 63u) : lane;
-                const bool won = pend && owner[pslot] == stamp;
+                const bool won = pend && owner[b.slot] == stamp;
                 const float gm = got ? 1.f : 0.f;
                 float gU[3], gV[3];
                 // every lane must execute the bpermute: it cannot read lanes that are inactive in EXEC
@@ -1455,7 +1450,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
                 for (int c = 0; c < 3; ++c) { gU[c] = gm * __shfl(rU[c], src); gV[c] = gm * __shfl(rV[c], src); }
                 const float gSig = gm * __shfl(rSig, src);
                 const float gRho = MODE == NLOSGR_MODE_NOOCL ? 0.f : gm * __shfl(rRho, src);
-                const int sij = __shfl(pij, src);
+                const int sij = __shfl(b.ij, src);
                 const int gij = got ? sij : 0;
                 const float2 th = tth[gij & 0xFFFF], ph = tph[gij >> 16];
                 const float d3[3] = {th.x * ph.x, th.x * ph.y, th.y};
@@ -1726,11 +1721,6 @@ void launch_bwd(const KArgs& ka, size_t shm, hipStream_t s) {
     dim3 grid((ka.g_hi - ka.g_lo + gpb - 1) / gpb, ka.nsplit);
     constexpr bool kCanTail = MODE == NLOSGR_MODE_NOOCL && !DENSE && !RAYS;
     const bool tail = kCanTail && ka.opt.cutoff >= kTailCutoff;
-    const char* nb = getenv("NLOSGR_BNBLK");   // A/B: non-blocking hand-off (NBLK)
-    if (tail && !ka.bshared && nb && nb[0] == '1') {
-        hipLaunchKernelGGL((bwd_kernel<PRESET, MODE, DENSE, RAYS, CACHE, false, kCanTail, true>), grid, dim3(kBlock), shm, s, ka);
-        return;
-    }
     if (ka.bshared) {
         if (tail) hipLaunchKernelGGL((bwd_kernel<PRESET, MODE, DENSE, RAYS, CACHE, true, kCanTail>), grid, dim3(kBlock), shm, s, ka);
         else hipLaunchKernelGGL((bwd_kernel<PRESET, MODE, DENSE, RAYS, CACHE, true>), grid, dim3(kBlock), shm, s, ka);

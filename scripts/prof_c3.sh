@@ -1,10 +1,10 @@
 # Round profile of the driver's bench command (bench.py --steps 20 --warmup 5, C3 defaults):
 # the bench line itself, a kernel-trace stats pass of the same command, then separate PMC passes
 # (FETCH_SIZE; WRITE_SIZE; SQ + GRBM; LDS) as MI355X_MICROARCH.md prescribes.  Output -> gpurun_out/prof_c3.
-#   PASSES="bench kt fetch write sq lds" bash scripts/prof_c3.sh [extra bench args]
+#   [OUT=gpurun_out/name] PASSES="bench kt fetch write sq lds" bash scripts/prof_c3.sh [extra bench args]
 set -o pipefail
 export TMPDIR=/tmp NLOSGR_BENCH_PROGRESS=1
-P=/tmp/prof_c3; O=gpurun_out/prof_c3; mkdir -p $P $O
+O=${OUT:-gpurun_out/prof_c3}; P=/tmp/$(basename $O); mkdir -p $P $O
 ARGS="--steps 20 --warmup 5 $*"
 PASSES=${PASSES:-"bench kt fetch write sq lds"}
 pass() {   # name, rocprofv3 options...
