@@ -167,8 +167,9 @@ class Snapshot:
 
 def timed_run(step, steps, warmup, world, dev):
     """W untimed steps, then EXACTLY K steps between barrier + synchronize on both sides; returns
-    the max-over-ranks wall time and each step's (fwd_ms, bwd_ms) from its HIP events (read after
-    the per-step synchronize, which the driver's contract keeps inside the timed region)."""
+    the max-over-ranks wall time and each step's (fwd_ms, bwd_ms) from its HIP events (step()
+    returns a callable read after the per-step synchronize, which the driver's contract keeps
+    inside the timed region)."""
     for _ in range(warmup):
         step()
     torch.cuda.synchronize(dev)
@@ -178,9 +179,9 @@ def timed_run(step, steps, warmup, world, dev):
     t0 = time.perf_counter()
     phases = []
     for i in range(steps):
-        ev_fwd, ev_bwd = step()
+        phase = step()
         torch.cuda.synchronize(dev)
-        phases.append((ev_fwd[0].elapsed_time(ev_fwd[1]), ev_bwd[0].elapsed_time(ev_bwd[1]) if ev_bwd else 0.0))
+        phases.append(phase())
         if PROGRESS:
             print(f"[bench] step {i + 1}/{steps} fwd {phases[-1][0]:.1f} ms bwd {phases[-1][1]:.1f} ms",
                   file=sys.stderr, flush=True)
@@ -280,9 +281,9 @@ def main():
                     ev_fwd[0].record(stream)
                     render_forward(*params, geo, cfg, True, False)
                     ev_fwd[1].record(stream)
-                    return ev_fwd, None
+                    return lambda: (ev_fwd[0].elapsed_time(ev_fwd[1]), 0.0)
                 train()
-                return ev_fwd, ev_bwd
+                return train.phase_ms   # HIP events of the step's phases (occl: summed over its batches)
 
             elapsed, evs = timed_run(step, a.steps, a.warmup, world, dev)
             fwd_ms = [e[0] for e in evs]

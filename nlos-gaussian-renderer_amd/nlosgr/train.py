@@ -14,6 +14,7 @@ host synchronisation inside the step:
 The returned loss is a device tensor; reading it is the caller's choice (and its only sync).
 """
 import math
+import os
 from dataclasses import dataclass, replace
 
 import torch
@@ -21,7 +22,11 @@ import torch.distributed as dist
 
 from . import _lib
 from .model import features_flat
-from .render import render_backward, render_forward, use_ray_cache
+from .render import render_backward, render_forward, tile_rows_bytes, use_ray_cache
+
+# occlusion mode: wall points per fused forward/MSE/backward batch are sized so that the batch's row
+# cache (the forward's (D, W) rows, reloaded by the backward) stays within this budget
+OCCL_BATCH_BYTES = int(float(os.environ.get("NLOSGR_OCCL_BATCH_GB", "8")) * 2 ** 30)
 
 GROUPS = ("mu", "f_dc", "f_rest", "opacity", "scaling", "rotation")   # gaussian_model.py:229-236
 
@@ -208,6 +213,7 @@ class TrainStep:
         self.events = events      # optional {"fwd": (start, end), "bwd": (start, end)} HIP events (bench timing)
         self.buckets = int(buckets)   # gradient all-reduce buckets overlapped with the backward (world > 1)
         self.iteration = 0
+        self._batch_events = []
         ng = model._mu.shape[0]
         self._tensors = [model._mu.data, model._features_dc.data.view(ng, -1), model._features_rest.data.view(ng, -1),
                          model._opacity.data.view(ng), model._scaling.data, model._rotation.data]
@@ -236,6 +242,59 @@ class TrainStep:
                          max_steps=o.position_lr_max_steps)     # update_learning_rate, gaussian_model.py:244-249
         return [mu_lr, o.feature_lr, o.feature_lr / 20.0, o.opacity_lr, o.scaling_lr, o.rotation_lr]
 
+    def occl_batches(self):
+        """Wall-point ranges [p0, p1) of the occlusion mode's fused batches (row cache <= OCCL_BATCH_BYTES)."""
+        P = self.geo.nwall
+        per = max(1, tile_rows_bytes(self.geo) // max(1, P))
+        nb = max(1, OCCL_BATCH_BYTES // per)
+        return [(p0, min(P, p0 + nb)) for p0 in range(0, P, nb)]
+
+    def phase_ms(self):
+        """(forward, backward) milliseconds of the last step from its HIP events (after a synchronize);
+        the occlusion mode's batches are summed per phase."""
+        ev = self.events
+        if self._batch_events:
+            f = sum(a.elapsed_time(b) for a, b, _, _ in self._batch_events)
+            g = sum(c.elapsed_time(d) for _, _, c, d in self._batch_events)
+            return f, g
+        return ev["fwd"][0].elapsed_time(ev["fwd"][1]), ev["bwd"][0].elapsed_time(ev["bwd"][1])
+
+    def _occl_step(self, args, cfg):
+        """Occlusion compositing (path C's shared transmittance): the wall is rendered in batches of
+        wall points; per batch the forward stores its tiles' (D, W) rows, the MSE gradient of the batch
+        follows at once (the loss is a sum over wall points) and the backward reloads the rows instead
+        of re-running the forward sweep, so the row cache is bounded by the batch (C3: 8 GiB of rows
+        per 1024 wall points instead of 128 GiB for the wall).  Returns (grads, loss4)."""
+        dev = args[0].device
+        stream = torch.cuda.current_stream(dev) if self.events else None
+        sums = torch.zeros(2, dtype=torch.float32, device=dev)
+        acc = None
+        params = args[:5]
+        for (p0, p1) in self.occl_batches():
+            geo = self.geo.slice(p0, p1) if (p0, p1) != (0, self.geo.nwall) else self.geo
+            evs = None
+            if self.events:
+                evs = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+                self._batch_events.append(tuple(evs))
+                evs[0].record(stream)
+            hist, _, ws = render_forward(*params, geo, cfg, True, False, ray_cache=True)
+            if evs:
+                evs[1].record(stream)
+            n_b = geo.nwall * geo.nr
+            loss4, grad = mse(hist, self.target[p0:p1], self.gt_times, grad_scale=n_b / self.n_total, raw=True)
+            sums += loss4[2:4]
+            if evs:
+                evs[2].record(stream)
+            d = render_backward(*params, geo, cfg, grad_hist=grad, workspace=ws, ray_cache=True)
+            if evs:
+                evs[3].record(stream)
+            del ws, hist, grad
+            acc = list(d) if acc is None else [a.add_(b) for a, b in zip(acc, d)]
+        d_mu, d_s, d_q, d_o, d_f = acc
+        se, st = sums[0], sums[1]
+        loss4 = torch.stack([se / float(self.n_total), torch.where(st > 0, se / st, torch.zeros_like(se)), se, st])
+        return [d_mu, d_f[:, :1], d_f[:, 1:], d_o, d_s, d_q], loss4
+
     def __call__(self, iteration=None):
         it = self.iteration if iteration is None else iteration
         m = self.model
@@ -243,6 +302,13 @@ class TrainStep:
         cfg = replace(self.cfg, sh_degree=int(m.active_sh_degree))
         feats = features_flat(m).detach().contiguous()
         args = (m._mu.detach(), m._scaling.detach(), m._rotation.detach(), m._opacity.detach(), feats, self.geo)
+        self._batch_events = []
+        if cfg.mode == "occl" and cfg.ray_cache:
+            grads, loss4 = self._occl_step(args, cfg)
+            loss2 = loss4[:2]
+            if self.world > 1:
+                grads, loss2 = allreduce_step(grads, loss4, self.n_total, self.group)
+            return self._finish(grads, loss2, it)
         cache = use_ray_cache(cfg, self.geo, ng)
         ev = self.events
         stream = torch.cuda.current_stream(m._mu.device) if ev else None
@@ -284,6 +350,10 @@ class TrainStep:
             grads = [d_mu, d_f[:, :1], d_f[:, 1:], d_o, d_s, d_q]
             if self.world > 1:
                 grads, loss2 = allreduce_step(grads, loss4, self.n_total, self.group)
+        return self._finish(grads, loss2, it)
+
+    def _finish(self, grads, loss2, it):
+        m = self.model
         if self.opt.regularization:
             # + opacity_reg mean|sigmoid(o)| + scale_reg mean|exp(s)| (main.py:204-208); replicated
             # terms, so added after the all-reduce.  equal_loss stays the render term's (as there).

@@ -257,3 +257,34 @@ def test_aabb_early_exit_exact():
     for a, b in zip(d_full, d_head):
         assert torch.equal(a[:300], b)
         assert float(a[300:].abs().max()) == 0.0
+
+
+@pytest.mark.parametrize("selection,cutoff", [("support", 5.7), ("aabb", 5.7)])
+def test_occl_batched_train_step_matches_whole_wall(monkeypatch, selection, cutoff):
+    """TrainStep's occlusion mode runs forward -> MSE -> backward per batch of wall points, the backward
+    reloading the batch's (D, W) rows (a row cache bounded by the batch).  Forced to batches of two
+    wall points, its gradients and loss equal the whole-wall composition without any cache: forward,
+    MSE over the whole volume, recomputing backward (sums in another order: rtol 1e-5)."""
+    from nlosgr import features_flat, train as T_
+    from nlosgr.geometry import build_geometry
+    from nlosgr.render import RenderConfig, render_backward, render_forward, tile_rows_bytes
+    walls, box = _scene()
+    m = _model(90, 3, 29, 1.0, 1.0)
+    geo = build_geometry(walls, box, NS, START, START + T, C, DELTAT, 0.5, "cuda", "occl")
+    cfg = RenderConfig(preset="cuda", mode="occl", sh_degree=3, cutoff=cutoff, c_deltaT=C * DELTAT,
+                       selection=selection)
+    g = torch.Generator().manual_seed(4)
+    target = (torch.rand(walls.shape[0], T, generator=g) * 1e-3).cuda()
+    args = (m._mu.detach(), m._scaling.detach(), m._rotation.detach(), m._opacity.detach(),
+            features_flat(m).detach().contiguous())
+    hist, _ = render_forward(*args, geo, cfg)
+    loss4, grad = T_.mse(hist, target, 100.0, raw=True)
+    ref = render_backward(*args, geo, cfg, grad_hist=grad)
+    ref = [ref[0], ref[4][:, :1], ref[4][:, 1:], ref[3], ref[1], ref[2]]
+    monkeypatch.setattr(T_, "OCCL_BATCH_BYTES", 2 * tile_rows_bytes(geo) // walls.shape[0])
+    step = T_.TrainStep(m, geo, cfg, target, gt_times=100.0, keep_grads=True)
+    assert len(step.occl_batches()) == (walls.shape[0] + 1) // 2 > 1
+    loss2 = step()
+    _close(loss2, loss4[:2], 1e-5, msg="loss")
+    for name, a, b in zip(T_.GROUPS, step.grads, ref):
+        _close(a, b.reshape(a.shape), 1e-5, atol=1e-12, msg=f"grad {name}")
