@@ -83,6 +83,8 @@ struct TArgs {
     long long nitems;
     int nslot;
     unsigned long long* diag;   // NLOSGR_TILES_DIAG: per-phase cycles of thread 0, summed over workgroups
+    unsigned long long* next;   // forward: dynamic item counter (items are independent; the backward keeps the
+                                // static schedule, whose slot-private accumulator rows need a fixed order)
     float2* rcache;          // OCCL row cache [nitems][rt][nr] (D, W) (opt.ray_cache): the forward's rows,
                              // reloaded by the backward instead of re-running its first sweep
 };
@@ -246,9 +248,22 @@ __global__ __launch_bounds__(tile_threads<BWD>()) void tile_kernel(TArgs k) {
         tc = t1;                                     \
     }
     if (kDiag && k.diag && tid == 0) tc = clock64();
-    for (long long item = blockIdx.x; item < k.nitems; item += k.nslot) {
+    __shared__ long long s_next;
+    // forward: a slot takes the next unclaimed item when it finishes one (per-item outputs, so the
+    // order does not matter); backward: items s, s + nslot, ... (fixed order of the slot's sums)
+    auto advance = [&](long long it) -> long long {
+        if (BWD || !k.next) return it + k.nslot;
+        __syncthreads();
+        if (tid == 0) s_next = (long long)k.nslot + (long long)atomicAdd(k.next, 1ull);
+        __syncthreads();
+        return s_next;
+    };
+    for (long long item = blockIdx.x; item < k.nitems; item = advance(item)) {
+        // item -> (wall point, tile), the tile index rotated by the wall point: with nslot a multiple of
+        // ntiles a slot's static items would otherwise all sit at one tile position of the angular grid
+        // (C3: slot s always tile s % 64, so the slots holding central tiles set the launch time)
         const int p = (int)(item / k.ntiles);
-        const int t = (int)(item - (long long)p * k.ntiles);
+        const int t = (int)((item - (long long)p * k.ntiles + p) % k.ntiles);
         const int ti0 = (t / k.ntile_j) * k.ti, tj0 = (t % k.ntile_j) * k.tj;
         const float px = k.geo.wall[3 * p], py = k.geo.wall[3 * p + 1], pz = k.geo.wall[3 * p + 2];
         const float* sth = k.geo.sin_theta + (size_t)p * nt;
@@ -898,7 +913,7 @@ int cu_count() {
 struct TPlan {
     int rt, ti, tj, nti, ntj, ntiles, nslot;
     long long nitems;
-    size_t off_cull, off_bbox, off_acc, off_hpart, off_rows, total;
+    size_t off_cull, off_bbox, off_acc, off_hpart, off_next, off_rows, total;
 };
 
 // the OCCL row cache: 8 B per (item, tile ray, bin), e.g. C3 (128x128 wall, 32x32 rays, 1024 bins) 128 GiB
@@ -922,7 +937,8 @@ TPlan plan(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_o
     P.off_bbox = P.off_cull + align_up(ng * sizeof(float4));
     P.off_acc = P.off_bbox + align_up(ng * 6 * sizeof(float));
     P.off_hpart = P.off_acc + align_up((size_t)P.nslot * ng * kRec * sizeof(float));
-    P.off_rows = P.off_hpart + align_up((size_t)geo->nwall * P.ntiles * geo->nr * sizeof(float));
+    P.off_next = P.off_hpart + align_up((size_t)geo->nwall * P.ntiles * geo->nr * sizeof(float));
+    P.off_rows = P.off_next + align_up(sizeof(unsigned long long));
     P.total = P.off_rows + (row_cache(opt) ? align_up((size_t)P.nitems * P.rt * geo->nr * sizeof(float2)) : 0);
     return P;
 }
@@ -984,6 +1000,7 @@ int prepare(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_
     a.ntile_i = P.nti; a.ntile_j = P.ntj; a.ntiles = P.ntiles;
     a.nitems = P.nitems; a.nslot = P.nslot;
     a.rcache = row_cache(opt) ? (float2*)(base + P.off_rows) : nullptr;
+    a.next = (unsigned long long*)(base + P.off_next);
     launch_preprocess(g, (GaussRec*)base, s);
     HIPCHK(hipGetLastError());
     const int nb = (g->ng + 255) / 256;
@@ -1014,7 +1031,7 @@ int tiles_validate(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const 
     if (opt->selection != NLOSGR_SELECT_SUPPORT && opt->selection != NLOSGR_SELECT_AABB)
         return set_err(NLOSGR_E_INVALID, "unknown selection");
     if (geo->nr > 4096) return set_err(NLOSGR_E_UNSUPPORTED, "occl / AABB engine: nr <= 4096");
-    if ((size_t)TLayout(tile_rays(geo->nr), geo->nr, tile_threads<false>(), false).total * 4 > 160 * 1024)
+    if ((size_t)TLayout(tile_rays(geo->nr), geo->nr, tile_threads<false>(), false).total * 4 + 16 > 160 * 1024)
         return set_err(NLOSGR_E_UNSUPPORTED, "occl / AABB engine: LDS budget");
     return NLOSGR_OK;
 }
@@ -1037,6 +1054,7 @@ int tiles_fwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosg
     if (rc) return rc;
     a.hist_out = hist_out;
     a.ray_out = ray_out;
+    HIPCHK(hipMemsetAsync(a.next, 0, sizeof(unsigned long long), s));
     const size_t shm = (size_t)TLayout(P.rt, geo->nr, tile_threads<false>(), false).total * sizeof(float);
     dispatch_tile<false>(a, shm, s);
     HIPCHK(hipGetLastError());
