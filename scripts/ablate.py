@@ -11,6 +11,7 @@ cfgname = sys.argv[1] if len(sys.argv) > 1 else 'C3'
 sizes = {'C3': (100_000, 128, 1024), 'S1': (20_000, 32, 512), 'C5B': (500_000, 256, 2048), 'C1': (1_000, 32, 128)}
 preset = os.environ.get('NLOSGR_ABLATE_PRESET', 'cuda')
 cutoff = float(os.environ.get('NLOSGR_ABLATE_CUTOFF', '3.0'))
+mode = os.environ.get('NLOSGR_ABLATE_MODE', 'noocl')
 ng, H, T = sizes[cfgname]
 dev = torch.device('cuda:0')
 scene = Scene(H=H, W=H, T=T, ns=32)
@@ -20,10 +21,10 @@ if cfgname == 'C5B':   # one rank's band of the 8-way C5 wall shard
     b0, b1 = wall_band(H * H, 0, 8)
     geo = scene.geometry(dev, preset, walls=scene.walls(dev)[b0:b1].contiguous())
 else:
-    geo = scene.geometry(dev, preset)
+    geo = scene.geometry(dev, preset, mode)
 f = features_flat(m).detach()
 args = (m._mu.detach(), m._scaling.detach(), m._rotation.detach(), m._opacity.detach(), f, geo)
-base = make_config(m, scene, preset, cutoff=cutoff)
+base = make_config(m, scene, preset, mode, cutoff=cutoff)
 res = {}
 for flags in (0, 4, 1, 2):
     cfg = dataclasses.replace(base, flags=flags)
@@ -40,4 +41,4 @@ for flags in (0, 64, 32, 4, 1, 2):
     render_backward(*args, cfg, grad_hist=grad, **kw); torch.cuda.synchronize()
     t0 = time.perf_counter(); render_backward(*args, cfg, grad_hist=grad, **kw); torch.cuda.synchronize()
     bres[flags] = (time.perf_counter() - t0) * 1000
-print(json.dumps({'config': cfgname, 'ray_cache': cache, 'fwd_ms_by_flags': res, 'bwd_ms_by_flags': bres}))
+print(json.dumps({'config': cfgname, 'mode': mode, 'cutoff': cutoff, 'ray_cache': cache, 'fwd_ms_by_flags': res, 'bwd_ms_by_flags': bres}))
