@@ -566,7 +566,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
             }
             if (!anymore && qcount == 0 && have) break;   // next Gaussians; segments carry over
             // claim distinct start keys (distinct addresses; vector drain: distinct start pairs)
-            constexpr bool QUAD = MODE == NLOSGR_MODE_NOOCL && !RAYS && !DENSE;
+            constexpr bool QUAD = (MODE == NLOSGR_MODE_NOOCL || (MODE == NLOSGR_MODE_NETF && TAIL)) && !RAYS && !DENSE;
             constexpr int VW = 2;   // bins per LDS read-add-write of the vector drain (float2)
             const int key = QUAD ? (d.pos / VW) : d.pos;
             if (act) owner[key] = (unsigned char)lane;
@@ -586,7 +586,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
                 // per-step mask switching).
                 const int o = d.pos & (VW - 1);
                 const int lim = remw + o;   // slot j is in the segment iff o <= j < lim
-                if (TAIL && win) {
+                if (TAIL && win && MODE == NLOSGR_MODE_NOOCL) {
                     const float t0 = t - (float)o;   // slot 0 = the even bin at or below pos
                     float cur = fast_exp2(fmaf(d.ga, t0 * t0, d.al));
                     float q = fast_exp2(d.ga * fmaf(2.f, t0, 1.f));
@@ -600,6 +600,39 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
                         const float v1 = cur;
                         cur *= q;
                         q *= cc;
+                        float2 x = hb2[kv];
+                        x.x += v0; x.y += v1;
+                        hb2[kv] = x;
+                        compiler_fence();
+                    }
+                } else if (TAIL && win) {
+                    // netf, TAIL: out_k = w c dT sin(theta) pdf_k T_k, T_{k+1} = T_k (exp(-sigma pdf_k c dT)
+                    // + 1e-7), two bins per float2 read-add-write; slot 0 before pos (o = 1, a segment's
+                    // first round) adds 0 and leaves T as it is
+                    const float t0 = t - (float)o;
+                    float cur = fast_exp2(fmaf(d.ga, t0 * t0, d.al));
+                    float q = fast_exp2(d.ga * fmaf(2.f, t0, 1.f));
+                    const float cc = fast_exp2(2.f * d.ga);
+                    const float nsc = -d.sc * (2.f * kHalfLog2e);   // exp(-sigma c dT pdf) = exp2(pdf nsc)
+                    float2* hb2 = reinterpret_cast<float2*>(hb);
+#pragma unroll
+                    for (int kv = 0; kv < kSteps / VW; ++kv) {
+                        const float p0 = cur;
+                        cur *= q;
+                        q *= cc;
+                        const float p1 = cur;
+                        cur *= q;
+                        q *= cc;
+                        const float f0 = fast_exp2(p0 * nsc) + 1e-7f;
+                        float v0 = d.wc * T * p0;
+                        if (kv == 0) {
+                            v0 = o ? 0.f : v0;
+                            T = o ? T : T * f0;
+                        } else {
+                            T *= f0;
+                        }
+                        const float v1 = d.wc * T * p1;
+                        T *= fast_exp2(p1 * nsc) + 1e-7f;
                         float2 x = hb2[kv];
                         x.x += v0; x.y += v1;
                         hb2[kv] = x;
@@ -1207,6 +1240,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
                     const int slot = e & 0xFF, i = (e >> 8) & 0xFFF, j = e >> 20;
                     act = bray_setup<MODE, DENSE>(pdat + slot * 16, tth[i], tph[j], slot, i, j, nr, mc2, r0, dr,
                                                   inv_dr, f0log2, b) && !(k.opt.flags & 4);  // flags 4: no bins
+                    if (MODE == NLOSGR_MODE_NETF && TAIL) b.T *= b.st;   // sin(theta) rides on T (BV rows)
                 }
                 const int ntake = min(nidle, qcount);
                 qhead = (qhead + ntake) & (kRQ - 1);
@@ -1222,7 +1256,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
                 const int remw = act ? b.rem : 0;
                 // BV: the round starts at the even bin at or below pos (float2 row reads, half the LDS
                 // instructions); slot j is bin (pos & ~1) + j, in the segment iff o <= j < remw + o
-                constexpr bool BV = MODE == NLOSGR_MODE_NOOCL && !RAYS && !DENSE;
+                constexpr bool BV = (MODE == NLOSGR_MODE_NOOCL || (MODE == NLOSGR_MODE_NETF && TAIL)) && !RAYS && !DENSE;
                 const int o = BV && act ? (b.pos & 1) : 0;
                 const float* gr = grow + (act ? b.pos - o : 0);
                 const float* gw = RAYS && gray ? gray + (size_t)((b.ij & 0xFFFF) * np_ + (b.ij >> 16)) * nr + b.pos
@@ -1311,12 +1345,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
                     const float kE = -cdt * (2.f * kHalfLog2e) * b.sigma, ncdt = -cdt, crho = cdt * b.rho;
                     // culled: pdf by the exp2 recurrence (kRecurrence), re-seeded per round
                     float cur = 0.f, rq = 0.f, rcc = 0.f;
+                    // TAIL: the recurrence starts at slot 0 = bin pos - o; inactive lanes get a zero seed
+                    const float kseed = TAIL ? kap - (float)o : kap;
                     if (!DENSE) {
-                        cur = fast_exp2(fmaf(b.c2, kap * kap, b.c0));
-                        rq = fast_exp2(b.c2 * fmaf(2.f, kap, 1.f));
+                        cur = fast_exp2(fmaf(b.c2, kseed * kseed, b.c0));
+                        rq = fast_exp2(b.c2 * fmaf(2.f, kseed, 1.f));
                         rcc = fast_exp2(2.f * b.c2);
+                        if (TAIL && !(act && b.rem > 0)) cur = 0.f;
                     }
-                    if (!DENSE && small_x) {
+                    if (!DENSE && (small_x || TAIL)) {   // (netf TAIL is launched only when small_x)
                         // c dT <= 1/64: x = sigma pdf c dT <= c dT, so exp(-x) = 1 - om_exp_small(x) (no
                         // exp) and a_j = -c dT e_j / (e_j + 1e-7) = -c dT / (1 + 1e-7 / e_j) is the constant
                         // a_c = -c dT / (1 + 1e-7) to 1e-7 x relative (no rcp): part B's sums become
@@ -1326,7 +1363,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
                         float UA0 = 0.f, UA1 = 0.f, UA2 = 0.f, UB0 = 0.f, UB1 = 0.f, UB2 = 0.f;
 #pragma unroll
                         for (int m = 0; m < kBSteps; ++m) {
-                            const bool in = m < remw;
+                            // TAIL: no segment-end mask (the bins past the end carry the Gaussian's exact
+                            // tail, as in the no-occlusion drains); only slot 0 before pos (o = 1) in a
+                            // segment's first round is inactive.  sin(theta) is folded into T (bray start).
+                            const bool in = TAIL ? !(m == 0 && o) : m < remw;
                             const float pdf = cur;
                             cur *= rq;
                             rq *= rcc;
@@ -1348,16 +1388,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
                             UB2 = fmaf(pin, (float)(m * m), UB2);
                             T *= in ? f : 1.f;
                         }
-                        // S_n += sum h (kap + m)^n, kap = the round's first bin offset
+                        // S_n += sum h (kb + m)^n, kb = the round's first bin offset
+                        const float kb = kseed;
                         const float sg = b.sigma, sgb = b.sigma * ac;
                         S0 = fmaf(sg, UA0, S0);
-                        S1 = fmaf(sg, fmaf(kap, UA0, UA1), S1);
-                        S2 = fmaf(sg, fmaf(kap, fmaf(kap, UA0, 2.f * UA1), UA2), S2);
+                        S1 = fmaf(sg, fmaf(kb, UA0, UA1), S1);
+                        S2 = fmaf(sg, fmaf(kb, fmaf(kb, UA0, 2.f * UA1), UA2), S2);
                         S0b = fmaf(sgb, UB0, S0b);
-                        S1b = fmaf(sgb, fmaf(kap, UB0, UB1), S1b);
-                        S2b = fmaf(sgb, fmaf(kap, fmaf(kap, UB0, 2.f * UB1), UB2), S2b);
+                        S1b = fmaf(sgb, fmaf(kb, UB0, UB1), S1b);
+                        S2b = fmaf(sgb, fmaf(kb, fmaf(kb, UB0, 2.f * UB1), UB2), S2b);
                         dsigb = fmaf(ac, UB0, dsigb);
-                        kap += (float)kBSteps;
+                        kap += (float)(kBSteps - o);
                     } else {
 #pragma unroll
                     for (int m = 0; m < kBSteps; ++m) {
@@ -1708,10 +1749,12 @@ int bwd_nsplit_ws(const nlosgr_gaussians* g, const nlosgr_geometry* geo0, const 
 template <int PRESET, int MODE, bool DENSE, bool RAYS, bool CACHE>
 void launch_fwd(const KArgs& ka, size_t shm, hipStream_t s) {
     const dim3 grid(ka.geo.nwall, ka.hpart ? ka.nfsplit : 1);
-    constexpr bool kCanTail = MODE == NLOSGR_MODE_NOOCL && !DENSE && !RAYS;
-    // NLOSGR_FTAIL=0: masked forward drain at every cutoff (A/B and parity cross-check)
+    constexpr bool kCanTail = (MODE == NLOSGR_MODE_NOOCL || MODE == NLOSGR_MODE_NETF) && !DENSE && !RAYS;
+    // NLOSGR_FTAIL=0: masked forward drain at every cutoff (A/B and parity cross-check); netf takes the
+    // TAIL drain where its backward does (c dT <= 1/64), so both see the same support
     const char* ftail = getenv("NLOSGR_FTAIL");
-    const bool tail = kCanTail && ka.opt.cutoff >= kTailCutoff && !ka.counts && !(ftail && ftail[0] == '0');
+    const bool tail = kCanTail && ka.opt.cutoff >= kTailCutoff && !ka.counts && !(ftail && ftail[0] == '0') &&
+                      (MODE != NLOSGR_MODE_NETF || ka.opt.c_deltaT <= kSmallX);
     if (tail) hipLaunchKernelGGL((fwd_kernel<PRESET, MODE, DENSE, RAYS, CACHE, kCanTail>), grid, dim3(kBlock), shm, s, ka);
     else hipLaunchKernelGGL((fwd_kernel<PRESET, MODE, DENSE, RAYS, CACHE>), grid, dim3(kBlock), shm, s, ka);
 }
@@ -1719,8 +1762,10 @@ template <int PRESET, int MODE, bool DENSE, bool RAYS, bool CACHE>
 void launch_bwd(const KArgs& ka, size_t shm, hipStream_t s) {
     const int gpb = ka.bshared ? kNB * kWaves : kNB;
     dim3 grid((ka.g_hi - ka.g_lo + gpb - 1) / gpb, ka.nsplit);
-    constexpr bool kCanTail = MODE == NLOSGR_MODE_NOOCL && !DENSE && !RAYS;
-    const bool tail = kCanTail && ka.opt.cutoff >= kTailCutoff;
+    constexpr bool kCanTail = (MODE == NLOSGR_MODE_NOOCL || MODE == NLOSGR_MODE_NETF) && !DENSE && !RAYS;
+    const char* bt = getenv("NLOSGR_BTAIL");   // NLOSGR_BTAIL=0: masked backward drains (A/B, parity cross-check)
+    const bool tail = kCanTail && ka.opt.cutoff >= kTailCutoff && !(bt && bt[0] == '0') &&
+                      (MODE != NLOSGR_MODE_NETF || ka.opt.c_deltaT <= kSmallX);
     if (ka.bshared) {
         if (tail) hipLaunchKernelGGL((bwd_kernel<PRESET, MODE, DENSE, RAYS, CACHE, true, kCanTail>), grid, dim3(kBlock), shm, s, ka);
         else hipLaunchKernelGGL((bwd_kernel<PRESET, MODE, DENSE, RAYS, CACHE, true>), grid, dim3(kBlock), shm, s, ka);

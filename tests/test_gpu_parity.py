@@ -106,7 +106,17 @@ def test_volume_vs_oracle_netf_small_cdt(preset, cutoff):
     _volume_vs_oracle(preset, "netf", cutoff, 3, T=96)
 
 
-def _volume_vs_oracle(preset, mode, cutoff, deg, T=40):
+@pytest.mark.parametrize("preset", ["torch", "cuda"])
+def test_netf_long_rays_opaque_late_gaussian(preset):
+    """netf over C3's radial grid (T = 1024 bins, c dT = 1.25e-3: the exp-free transmittance and the
+    one-pass backward, whose per-bin suffix term a_j (E - P_j) is formed as A + E B; at cutoff >= 5 also
+    the mask-free TAIL drains) with a near-opaque Gaussian (sigmoid(o) ~ 0.98) placed late on the rays,
+    where the prefix P_j comes close to the ray's total E: forward and all gradients vs the oracle."""
+    for cutoff in (5.7, 3.0):
+        _volume_vs_oracle(preset, "netf", cutoff, 3, T=1024, opaque_late=True)
+
+
+def _volume_vs_oracle(preset, mode, cutoff, deg, T=40, opaque_late=False):
     from nlosgr import GaussianParams, features_flat
     from nlosgr.geometry import build_geometry, relay_wall_grid, volume_box_point
     from nlosgr.render import RenderConfig, render
@@ -119,6 +129,10 @@ def _volume_vs_oracle(preset, mode, cutoff, deg, T=40):
         with torch.no_grad():
             model._scaling.add_(1.2)
     walls = relay_wall_grid(2, 3, device=dev)
+    if opaque_late:   # the Gaussian farthest from the wall's centre made near-opaque
+        with torch.no_grad():
+            far = int((model._mu - walls.mean(0)).norm(dim=1).argmax())
+            model._opacity[far] = 4.0
     box = volume_box_point((0.0, 0.5, 0.0), 0.5, dev)
     geo = build_geometry(walls, box, ns, start, end, c, deltaT, 0.5, preset, mode)
     cfg = RenderConfig(preset=preset, mode=mode, sh_degree=deg, cutoff=cutoff, c_deltaT=c * deltaT)
