@@ -480,6 +480,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
     float* rout = RAYS ? k.ray_out + (size_t)p * nt * np_ * nr : nullptr;
     const float rscale = k.opt.ray_scale;
     const int flags = k.opt.flags;
+    // the float2 drain (two bins per LDS read-add-write; claim keys on bin pairs)
+    constexpr bool QUADF = (MODE == NLOSGR_MODE_NOOCL || (MODE == NLOSGR_MODE_NETF && TAIL)) && !RAYS && !DENSE;
     const int pad = nr + kSteps + lane;       // this lane's private pad bins (non-winners)
     const int padq = al4(nr + kSteps);        // quad drain: one pad quad row shared by non-winners (they add 0)
     unsigned npair = 0, nseg = 0;
@@ -552,6 +554,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
                     got = drain_setup<MODE, DENSE, RAYS>(A, u0, lws, scs, wcs, tth[i], tph[j], i, j, np_, nr, mc2,
                                                          r0, dr, inv_dr, f0log2, d, stag);
                     if (got) nsamp += (unsigned)(d.rem + (dense_wrap<MODE, DENSE>() ? d.wrap : 0));
+                    if (MODE == NLOSGR_MODE_NETF && TAIL && QUADF) d.T *= d.wc;   // the weight rides on T
                     act = got && !(flags & 4);    // diagnostics: segment records only
                 }
                 nseg += __popcll(__builtin_amdgcn_ballot_w64(got));
@@ -566,7 +569,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
             }
             if (!anymore && qcount == 0 && have) break;   // next Gaussians; segments carry over
             // claim distinct start keys (distinct addresses; vector drain: distinct start pairs)
-            constexpr bool QUAD = (MODE == NLOSGR_MODE_NOOCL || (MODE == NLOSGR_MODE_NETF && TAIL)) && !RAYS && !DENSE;
+            constexpr bool QUAD = QUADF;
             constexpr int VW = 2;   // bins per LDS read-add-write of the vector drain (float2)
             const int key = QUAD ? (d.pos / VW) : d.pos;
             if (act) owner[key] = (unsigned char)lane;
@@ -624,14 +627,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
                         cur *= q;
                         q *= cc;
                         const float f0 = fast_exp2(p0 * nsc) + 1e-7f;
-                        float v0 = d.wc * T * p0;
+                        float v0 = T * p0;   // T carries w c dT sin(theta) (set at the segment's start)
                         if (kv == 0) {
                             v0 = o ? 0.f : v0;
                             T = o ? T : T * f0;
                         } else {
                             T *= f0;
                         }
-                        const float v1 = d.wc * T * p1;
+                        const float v1 = T * p1;
                         T *= fast_exp2(p1 * nsc) + 1e-7f;
                         float2 x = hb2[kv];
                         x.x += v0; x.y += v1;
@@ -924,6 +927,9 @@ __global__ __launch_bounds__(kBlock) void fwd_dense_kernel(KArgs k) {
 #define NLOSGR_BSTEPS 24
 #endif
 constexpr int kBSteps = NLOSGR_BSTEPS;   // bins per lane per backward drain round
+#ifndef NLOSGR_BSTEPS_NETF
+#define NLOSGR_BSTEPS_NETF 16
+#endif
 constexpr int kBwdSlots = 13;   // per-Gaussian backward partial: dA[9], dMu[3], dsigma (stride 32 in HBM)
 constexpr int kShPart = 28;     // sh_kernel partial: dF[KM <= 25], dMu[3] (at KM), pad
 
@@ -1079,6 +1085,9 @@ __device__ __forceinline__ bool bray_setup(const float* pd, float2 th, float2 ph
 
 template <int PRESET, int MODE, bool DENSE, bool RAYS, bool CACHE, bool SHR, bool TAIL = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) void bwd_kernel(KArgs k) {
+    // bins per drain round: netf keeps more per-ray state, so its rounds are shorter (no spill at 128 VGPRs)
+    constexpr int kRS = MODE == NLOSGR_MODE_NETF ? NLOSGR_BSTEPS_NETF : kBSteps;
+    static_assert(kRS <= kBSteps && kRS % 2 == 0, "the staged row is padded by kBSteps bins");
     extern __shared__ __align__(16) float smem[];
     const int nr = k.geo.nr, nt = k.geo.nt, np_ = k.geo.np;
     constexpr bool shr = SHR;   // == (k.bshared != 0)
@@ -1261,16 +1270,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
                 const float* gr = grow + (act ? b.pos - o : 0);
                 const float* gw = RAYS && gray ? gray + (size_t)((b.ij & 0xFFFF) * np_ + (b.ij >> 16)) * nr + b.pos
                                                : nullptr;
-                float Hs[kBSteps];
+                float Hs[kRS];
                 if (BV && TAIL) {
                     // no end mask: a segment's last round also weighs the bins past its end (up to
-                    // kBSteps - 1 of them) with their exact pdf, < exp(-m_c^2 / 2) of the Gaussian's peak
+                    // kRS - 1 of them) with their exact pdf, < exp(-m_c^2 / 2) of the Gaussian's peak
                     // (<= 3.7e-6 at m_c >= kTailCutoff: the support is a superset of the forward's, closer
                     // to the dense reference; idle and blocked lanes are zeroed through their pdf seed
                     // below).  Slot 0 before pos (o = 1) stays masked: the recurrence starts at pos.
                     const float2* g2 = reinterpret_cast<const float2*>(gr);
 #pragma unroll
-                    for (int m = 0; m < kBSteps; m += 2) {
+                    for (int m = 0; m < kRS; m += 2) {
                         const float2 h = g2[m / 2];
                         Hs[m] = (m == 0 && o) ? 0.f : h.x;
                         Hs[m + 1] = h.y;
@@ -1279,14 +1288,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
                     const int lim = remw + o;
                     const float2* g2 = reinterpret_cast<const float2*>(gr);
 #pragma unroll
-                    for (int m = 0; m < kBSteps; m += 2) {
+                    for (int m = 0; m < kRS; m += 2) {
                         const float2 h = g2[m / 2];
                         Hs[m] = (m >= o && m < lim) ? h.x : 0.f;
                         Hs[m + 1] = (m + 1 < lim) ? h.y : 0.f;
                     }
                 } else {
 #pragma unroll
-                    for (int m = 0; m < kBSteps; ++m) {
+                    for (int m = 0; m < kRS; ++m) {
                         float H = gr[m];
                         if (RAYS || MODE == NLOSGR_MODE_NETF) H *= b.st;
                         if (RAYS && gw && m < remw) H += gw[m] * rscale;
@@ -1307,7 +1316,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
                         const float cc = fast_exp2(2.f * b.c2);
                         float U0 = 0.f, U1 = 0.f, U2 = 0.f;
 #pragma unroll
-                        for (int m = 0; m < kBSteps; ++m) {
+                        for (int m = 0; m < kRS; ++m) {
                             const float hp = Hs[m] * pdf;
                             U0 += hp;
                             U1 = fmaf(hp, (float)m, U1);
@@ -1324,10 +1333,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
                         S0 += U0;
                         S1 += fmaf(kb, U0, U1);
                         S2 += fmaf(kb, fmaf(kb, U0, 2.f * U1), U2);
-                        kap += (float)(kBSteps - o);
+                        kap += (float)(kRS - o);
                     } else
 #pragma unroll
-                    for (int m = 0; m < kBSteps; ++m) {
+                    for (int m = 0; m < kRS; ++m) {
                         const float hp = Hs[m] * fast_exp2(fmaf(b.c2, kap * kap, b.c0));
                         const float t1 = hp * kap;
                         S0 += hp; S1 += t1; S2 = fmaf(t1, kap, S2);
@@ -1360,9 +1369,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
                         // a_c sum pdf (1, m, m^2) (moments about the round's first bin, like U_n above)
                         const float sx = cdt * b.sigma;
                         const float ac = ncdt / (1.0f + 1e-7f);
+                        // the prefix P_j = rho sum_{k<=j} H_k T_k x_k = rho drho_j (rho is the pair's), so part
+                        // A's weight is c rho H_j T_j - P_j a_c = crho HT + k1 drho; sum_j c1_j pdf_j (dsigma's
+                        // part A) is UA0, summed per round below
+                        const float k1 = -b.rho * ac;
                         float UA0 = 0.f, UA1 = 0.f, UA2 = 0.f, UB0 = 0.f, UB1 = 0.f, UB2 = 0.f;
 #pragma unroll
-                        for (int m = 0; m < kBSteps; ++m) {
+                        for (int m = 0; m < kRS; ++m) {
                             // TAIL: no segment-end mask (the bins past the end carry the Gaussian's exact
                             // tail, as in the no-occlusion drains); only slot 0 before pos (o = 1) in a
                             // segment's first round is inactive.  sin(theta) is folded into T (bray start).
@@ -1371,14 +1384,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
                             cur *= rq;
                             rq *= rcc;
                             const float x = pdf * sx;                 // sigma pdf c dT
-                            const float f = (1.0f - om_exp_small(x)) + 1e-7f;
+                            // exp(-x) + 1e-7 for x <= 1/64 (the x^4 / 24 term, <= 2.5e-9, is dropped)
+                            const float f = fmaf(x, fmaf(x, fmaf(x, -1.0f / 6.0f, 0.5f), -1.0f), 1.0f) + 1e-7f;
                             const float HT = Hs[m] * T;
                             const float hdt = HT * x;
                             drho += hdt;
-                            pre = fmaf(b.rho, hdt, pre);
-                            const float c1 = in ? fmaf(-pre, ac, crho * HT) : 0.f;
+                            const float c1 = in ? fmaf(k1, drho, crho * HT) : 0.f;
                             const float pin = in ? pdf : 0.f;
-                            dsig = fmaf(c1, pdf, dsig);
                             const float hA = c1 * pdf;                // x sigma at the end
                             UA0 += hA;
                             UA1 = fmaf(hA, (float)m, UA1);
@@ -1388,6 +1400,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
                             UB2 = fmaf(pin, (float)(m * m), UB2);
                             T *= in ? f : 1.f;
                         }
+                        dsig += UA0;
+                        pre = b.rho * drho;
                         // S_n += sum h (kb + m)^n, kb = the round's first bin offset
                         const float kb = kseed;
                         const float sg = b.sigma, sgb = b.sigma * ac;
@@ -1398,10 +1412,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
                         S1b = fmaf(sgb, fmaf(kb, UB0, UB1), S1b);
                         S2b = fmaf(sgb, fmaf(kb, fmaf(kb, UB0, 2.f * UB1), UB2), S2b);
                         dsigb = fmaf(ac, UB0, dsigb);
-                        kap += (float)(kBSteps - o);
+                        kap += (float)(kRS - o);
                     } else {
 #pragma unroll
-                    for (int m = 0; m < kBSteps; ++m) {
+                    for (int m = 0; m < kRS; ++m) {
                         const bool in = m < remw;
                         float pdf;
                         if (DENSE) {
@@ -1439,8 +1453,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
                 if (act) {
                     if (b.rem > 0) {   // (a blocked lane, rem <= 0, added zeros and stays put)
                         b.kap = kap;
-                        b.pos += kBSteps - o;
-                        b.rem -= kBSteps - o;
+                        b.pos += kRS - o;
+                        b.rem -= kRS - o;
                     }
                     if (b.rem <= 0 && !pend) {
                         // pdf = exp(-|z|^2/2), z = z* + dl v:  dL/du0 = -sum P z,  dL/dv = -sum P dl z
