@@ -436,11 +436,11 @@ __device__ __forceinline__ void enumerate_cached(unsigned long long& bits0, unsi
 
 __device__ __forceinline__ void compiler_fence() { __asm__ __volatile__("" ::: "memory"); }
 
-// TAIL (culled no-occlusion histogram at cutoff >= kTailCutoff): the forward drain adds no masks.  A
-// round starts the recurrence at the even bin at or below pos and adds all kSteps values: the bins
-// before pos (one, o = 1) and past the segment's end (up to kSteps - 1) get their exact Gaussian
-// values, each < exp(-m_c^2 / 2) of the Gaussian's peak (<= 3.7e-6 at m_c >= kTailCutoff), so the
-// result lies between the culled and the dense sum.  Bins past nr land in the zeroed pad row.
+// TAIL (culled histogram at cutoff >= kTailCutoff): the forward drain has no end mask.  A round adds
+// kSteps values from the even bin at or below pos (a bin before pos, o = 1, adds 0): the bins past the
+// segment's end (up to kSteps - 1) get their exact Gaussian values, each < exp(-m_c^2 / 2) of the
+// Gaussian's peak (<= 3.7e-6 at m_c >= kTailCutoff), so the result lies between the culled and the
+// dense sum.  Bins past nr land in the zeroed pad row.
 constexpr float kTailCutoff = 5.0f;
 
 template <int PRESET, int MODE, bool DENSE, bool RAYS, bool CACHE, bool TAIL = false>
@@ -590,16 +590,22 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
                 const int o = d.pos & (VW - 1);
                 const int lim = remw + o;   // slot j is in the segment iff o <= j < lim
                 if (TAIL && win && MODE == NLOSGR_MODE_NOOCL) {
-                    const float t0 = t - (float)o;   // slot 0 = the even bin at or below pos
-                    float cur = fast_exp2(fmaf(d.ga, t0 * t0, d.al));
-                    float q = fast_exp2(d.ga * fmaf(2.f, t0, 1.f));
+                    // the recurrence is seeded at pos (inside the support: a seed one bin further out can
+                    // underflow for Gaussians much narrower than a bin); slot 0 before pos (o = 1) adds 0
+                    float cur = fast_exp2(fmaf(d.ga, t * t, d.al));
+                    float q = fast_exp2(d.ga * fmaf(2.f, t, 1.f));
                     const float cc = fast_exp2(2.f * d.ga);
                     float2* hb2 = reinterpret_cast<float2*>(hb);
 #pragma unroll
                     for (int kv = 0; kv < kSteps / VW; ++kv) {
-                        const float v0 = cur;
-                        cur *= q;
-                        q *= cc;
+                        const float v0 = (kv == 0 && o) ? 0.f : cur;
+                        if (kv == 0) {
+                            cur = o ? cur : cur * q;
+                            q = o ? q : q * cc;
+                        } else {
+                            cur *= q;
+                            q *= cc;
+                        }
                         const float v1 = cur;
                         cur *= q;
                         q *= cc;
@@ -612,17 +618,21 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
                     // netf, TAIL: out_k = w c dT sin(theta) pdf_k T_k, T_{k+1} = T_k (exp(-sigma pdf_k c dT)
                     // + 1e-7), two bins per float2 read-add-write; slot 0 before pos (o = 1, a segment's
                     // first round) adds 0 and leaves T as it is
-                    const float t0 = t - (float)o;
-                    float cur = fast_exp2(fmaf(d.ga, t0 * t0, d.al));
-                    float q = fast_exp2(d.ga * fmaf(2.f, t0, 1.f));
+                    float cur = fast_exp2(fmaf(d.ga, t * t, d.al));   // seeded at pos (see above)
+                    float q = fast_exp2(d.ga * fmaf(2.f, t, 1.f));
                     const float cc = fast_exp2(2.f * d.ga);
                     const float nsc = -d.sc * (2.f * kHalfLog2e);   // exp(-sigma c dT pdf) = exp2(pdf nsc)
                     float2* hb2 = reinterpret_cast<float2*>(hb);
 #pragma unroll
                     for (int kv = 0; kv < kSteps / VW; ++kv) {
                         const float p0 = cur;
-                        cur *= q;
-                        q *= cc;
+                        if (kv == 0) {
+                            cur = o ? cur : cur * q;
+                            q = o ? q : q * cc;
+                        } else {
+                            cur *= q;
+                            q *= cc;
+                        }
                         const float p1 = cur;
                         cur *= q;
                         q *= cc;
@@ -1266,12 +1276,28 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
                 // BV: the round starts at the even bin at or below pos (float2 row reads, half the LDS
                 // instructions); slot j is bin (pos & ~1) + j, in the segment iff o <= j < remw + o
                 constexpr bool BV = (MODE == NLOSGR_MODE_NOOCL || (MODE == NLOSGR_MODE_NETF && TAIL)) && !RAYS && !DENSE;
-                const int o = BV && act ? (b.pos & 1) : 0;
+                // BV4 (no-occlusion TAIL): the round starts at the bin at or below pos that is a multiple of
+                // 4 and reads the row as float4 (ds_read_b128: 16-lane groups over 16 bank quads conflict
+                // less per bin than 32-lane groups over 32 bank pairs, and half the instructions)
+                constexpr bool BV4 = MODE == NLOSGR_MODE_NOOCL && TAIL && !RAYS && !DENSE;
+                constexpr int BVW = BV4 ? 4 : 2;
+                const int o = BV && act ? (b.pos & (BVW - 1)) : 0;
                 const float* gr = grow + (act ? b.pos - o : 0);
                 const float* gw = RAYS && gray ? gray + (size_t)((b.ij & 0xFFFF) * np_ + (b.ij >> 16)) * nr + b.pos
                                                : nullptr;
                 float Hs[kRS];
-                if (BV && TAIL) {
+                if (BV4) {
+                    // as below, with slots 0..o-1 before pos masked (o <= 3)
+                    const float4* g4 = reinterpret_cast<const float4*>(gr);
+#pragma unroll
+                    for (int m = 0; m < kRS; m += 4) {
+                        const float4 h = g4[m / 4];
+                        Hs[m] = (m == 0 && o > 0) ? 0.f : h.x;
+                        Hs[m + 1] = (m == 0 && o > 1) ? 0.f : h.y;
+                        Hs[m + 2] = (m == 0 && o > 2) ? 0.f : h.z;
+                        Hs[m + 3] = h.w;
+                    }
+                } else if (BV && TAIL) {
                     // no end mask: a segment's last round also weighs the bins past its end (up to
                     // kRS - 1 of them) with their exact pdf, < exp(-m_c^2 / 2) of the Gaussian's peak
                     // (<= 3.7e-6 at m_c >= kTailCutoff: the support is a superset of the forward's, closer
@@ -1321,9 +1347,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
                             U0 += hp;
                             U1 = fmaf(hp, (float)m, U1);
                             U2 = fmaf(hp, (float)(m * m), U2);
-                            if (BV && m == 0) {   // the recurrence starts at pos (slot o)
-                                pdf = o ? pdf : pdf * q;
-                                q = o ? q : q * cc;
+                            if (BV && m < BVW - 1) {   // the recurrence starts at pos (slot o)
+                                pdf = m < o ? pdf : pdf * q;
+                                q = m < o ? q : q * cc;
                             } else {
                                 pdf *= q;
                                 q *= cc;

@@ -116,7 +116,16 @@ def test_netf_long_rays_opaque_late_gaussian(preset):
         _volume_vs_oracle(preset, "netf", cutoff, 3, T=1024, opaque_late=True)
 
 
-def _volume_vs_oracle(preset, mode, cutoff, deg, T=40, opaque_late=False):
+@pytest.mark.parametrize("mode", ["noocl", "netf"])
+def test_tail_drains_narrow_gaussians(mode):
+    """Gaussians much narrower than a bin (sigma ~ 0.05-0.3 bin along the rays) at 5.7 sigma, where the
+    TAIL drains (cutoff >= 5) run: their recurrences are seeded inside the support, so no seed
+    underflows and zeroes a round; forward and gradients vs the oracle (T = 96: c dT <= 1/64, so netf
+    takes its TAIL drains too)."""
+    _volume_vs_oracle("cuda", mode, 5.7, 3, T=96, scale_shift=-3.5)
+
+
+def _volume_vs_oracle(preset, mode, cutoff, deg, T=40, opaque_late=False, scale_shift=None):
     from nlosgr import GaussianParams, features_flat
     from nlosgr.geometry import build_geometry, relay_wall_grid, volume_box_point
     from nlosgr.render import RenderConfig, render
@@ -127,7 +136,7 @@ def _volume_vs_oracle(preset, mode, cutoff, deg, T=40, opaque_late=False):
     model = GaussianParams.synthetic(ng, deg, preset=preset, device=dev, seed=3)
     if preset == "cuda":   # make them large enough to cross several rays/bins at this coarse grid
         with torch.no_grad():
-            model._scaling.add_(1.2)
+            model._scaling.add_(1.2 if scale_shift is None else scale_shift)
     walls = relay_wall_grid(2, 3, device=dev)
     if opaque_late:   # the Gaussian farthest from the wall's centre made near-opaque
         with torch.no_grad():
