@@ -83,6 +83,7 @@ struct TArgs {
     long long nitems;
     int nslot;
     unsigned long long* diag;   // NLOSGR_TILES_DIAG: per-phase cycles of thread 0, summed over workgroups
+    int pbase;               // global index of wall point 0 of this launch (forward wall-point batches)
     unsigned long long* next;   // forward: dynamic item counter (items are independent; the backward keeps the
                                 // static schedule, whose slot-private accumulator rows need a fixed order)
     float2* rcache;          // OCCL row cache [nitems][rt][nr] (D, W) (opt.ray_cache): the forward's rows,
@@ -263,7 +264,7 @@ __global__ __launch_bounds__(tile_threads<BWD>()) void tile_kernel(TArgs k) {
         // ntiles a slot's static items would otherwise all sit at one tile position of the angular grid
         // (C3: slot s always tile s % 64, so the slots holding central tiles set the launch time)
         const int p = (int)(item / k.ntiles);
-        const int t = (int)((item - (long long)p * k.ntiles + p) % k.ntiles);
+        const int t = (int)((item - (long long)p * k.ntiles + p + k.pbase) % k.ntiles);
         const int ti0 = (t / k.ntile_j) * k.ti, tj0 = (t % k.ntile_j) * k.tj;
         const float px = k.geo.wall[3 * p], py = k.geo.wall[3 * p + 1], pz = k.geo.wall[3 * p + 2];
         const float* sth = k.geo.sin_theta + (size_t)p * nt;
@@ -899,6 +900,8 @@ __global__ __launch_bounds__(256) void tiles_finish_kernel(TArgs k, float* d_mu,
     chain_to_raw<NLOSGR_PRESET_CUDA>(k.g, i, a, d_scaling, d_rot);
 }
 
+constexpr size_t kHpartBytes = (size_t)1 << 30;   // forward tile partials per launch (1 GiB)
+
 int cu_count() {
     static int n = 0;
     if (n == 0) {
@@ -912,6 +915,7 @@ int cu_count() {
 
 struct TPlan {
     int rt, ti, tj, nti, ntj, ntiles, nslot;
+    int pbatch;              // forward: wall points per launch (the tile partials [pbatch][ntiles][nr] stay bounded)
     long long nitems;
     size_t off_cull, off_bbox, off_acc, off_hpart, off_next, off_rows, total;
 };
@@ -937,7 +941,16 @@ TPlan plan(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_o
     P.off_bbox = P.off_cull + align_up(ng * sizeof(float4));
     P.off_acc = P.off_bbox + align_up(ng * 6 * sizeof(float));
     P.off_hpart = P.off_acc + align_up((size_t)P.nslot * ng * kRec * sizeof(float));
-    P.off_next = P.off_hpart + align_up((size_t)geo->nwall * P.ntiles * geo->nr * sizeof(float));
+    // forward tile partials per launch: at most kHpartBytes (C5 with AABB selection: 65536 wall points x
+    // 128 tiles x 2048 bins would be 69 GB for the whole wall), so the forward runs in wall-point batches
+    const size_t per_wall = (size_t)P.ntiles * geo->nr * sizeof(float);
+    const char* hm = getenv("NLOSGR_TILE_HPART_MB");   // override (tests: force wall-point batches)
+    const size_t budget = hm ? (size_t)(atof(hm) * 1048576.0) : kHpartBytes;
+    long long pb = per_wall ? (long long)(budget / per_wall) : geo->nwall;
+    if (pb < 1) pb = 1;
+    P.pbatch = (int)(pb < geo->nwall ? pb : geo->nwall);
+    if (P.pbatch < 1) P.pbatch = 1;
+    P.off_next = P.off_hpart + align_up((size_t)P.pbatch * per_wall);
     P.off_rows = P.off_next + align_up(sizeof(unsigned long long));
     P.total = P.off_rows + (row_cache(opt) ? align_up((size_t)P.nitems * P.rt * geo->nr * sizeof(float2)) : 0);
     return P;
@@ -1052,17 +1065,37 @@ int tiles_fwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosg
     TArgs a;
     int rc = prepare(g, geo, opt, ws, P, a, s);
     if (rc) return rc;
-    a.hist_out = hist_out;
-    a.ray_out = ray_out;
-    HIPCHK(hipMemsetAsync(a.next, 0, sizeof(unsigned long long), s));
     const size_t shm = (size_t)TLayout(P.rt, geo->nr, tile_threads<false>(), false).total * sizeof(float);
-    dispatch_tile<false>(a, shm, s);
-    HIPCHK(hipGetLastError());
-    if (hist_out) {
-        const long long n = (long long)geo->nwall * geo->nr;
-        hipLaunchKernelGGL(tiles_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a.hpart, P.ntiles,
-                           (long long)geo->nwall, geo->nr, geo->att, geo->hscale, hist_out);
+    const int nt = geo->nt, np_ = geo->np, nr = geo->nr;
+    float2* rc0 = a.rcache;
+    // wall-point batches: one launch each over the batch's items (pointer offsets into the tables, the
+    // outputs and the row cache), so the tile partials stay within kHpartBytes
+    for (int p0 = 0; p0 < geo->nwall; p0 += P.pbatch) {
+        const int pn = geo->nwall - p0 < P.pbatch ? geo->nwall - p0 : P.pbatch;
+        TArgs b = a;
+        b.geo.nwall = pn;
+        b.geo.wall = geo->wall + 3 * (size_t)p0;
+        b.geo.sin_theta = geo->sin_theta + (size_t)p0 * nt;
+        b.geo.cos_theta = geo->cos_theta + (size_t)p0 * nt;
+        b.geo.sin_phi = geo->sin_phi + (size_t)p0 * np_;
+        b.geo.cos_phi = geo->cos_phi + (size_t)p0 * np_;
+        b.geo.grid_lin = geo->grid_lin + 4 * (size_t)p0;
+        b.geo.hscale = geo->hscale + p0;
+        b.nitems = (long long)pn * P.ntiles;
+        b.pbase = p0;   // the tile rotation follows the global wall index (the backward's row-cache items)
+        b.nslot = (int)(b.nitems < P.nslot ? b.nitems : P.nslot);
+        b.hist_out = hist_out;
+        b.ray_out = ray_out ? ray_out + (size_t)p0 * nt * np_ * nr : nullptr;
+        b.rcache = rc0 ? rc0 + (size_t)p0 * P.ntiles * P.rt * nr : nullptr;
+        HIPCHK(hipMemsetAsync(b.next, 0, sizeof(unsigned long long), s));
+        dispatch_tile<false>(b, shm, s);
         HIPCHK(hipGetLastError());
+        if (hist_out) {
+            const long long n = (long long)pn * nr;
+            hipLaunchKernelGGL(tiles_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, b.hpart,
+                               P.ntiles, (long long)pn, nr, geo->att, b.geo.hscale, hist_out + (size_t)p0 * nr);
+            HIPCHK(hipGetLastError());
+        }
     }
     return NLOSGR_OK;
 }

@@ -288,3 +288,32 @@ def test_occl_batched_train_step_matches_whole_wall(monkeypatch, selection, cuto
     _close(loss2, loss4[:2], 1e-5, msg="loss")
     for name, a, b in zip(T_.GROUPS, step.grads, ref):
         _close(a, b.reshape(a.shape), 1e-5, atol=1e-12, msg=f"grad {name}")
+
+
+@pytest.mark.parametrize("mode,selection", [("occl", "support"), ("noocl", "aabb")])
+def test_tile_forward_wall_batches_bitwise(monkeypatch, mode, selection):
+    """The ray-tile forward runs in wall-point batches once its tile partials would pass
+    NLOSGR_TILE_HPART_MB (1 GiB: C5 with AABB selection would need 69 GB for the wall).  Batches of one
+    wall point give bitwise the same histogram, per-ray output and (occlusion, row cache) gradients."""
+    from nlosgr import features_flat
+    from nlosgr.geometry import build_geometry
+    from nlosgr.render import RenderConfig, render_backward, render_forward
+    walls, box = _scene()
+    m = _model(90, 3, 31, 1.0, 1.0)
+    geo = build_geometry(walls, box, NS, START, START + T, C, DELTAT, 0.5, "cuda", mode)
+    cfg = RenderConfig(preset="cuda", mode=mode, sh_degree=3, cutoff=5.7, c_deltaT=C * DELTAT,
+                       ray_scale=1.0 if mode == "occl" else C * DELTAT, selection=selection)
+    args = (m._mu, m._scaling, m._rotation, m._opacity, features_flat(m).detach())
+    out = []
+    for hp in (None, "0.0001"):
+        if hp:
+            monkeypatch.setenv("NLOSGR_TILE_HPART_MB", hp)
+        h, r, ws = render_forward(*args, geo, cfg, want_rays=True, ray_cache=mode == "occl") \
+            if mode == "occl" else (*render_forward(*args, geo, cfg, want_rays=True), None)
+        gh = torch.ones_like(h)
+        d = render_backward(*args, geo, cfg, grad_hist=gh, workspace=ws, ray_cache=ws is not None)
+        out.append((h, r, d))
+    (h0, r0, d0), (h1, r1, d1) = out
+    assert torch.equal(h0, h1) and torch.equal(r0, r1)
+    for a, b in zip(d0, d1):
+        assert torch.equal(a, b)
