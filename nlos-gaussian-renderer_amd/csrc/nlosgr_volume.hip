@@ -972,7 +972,7 @@ struct BwdLayout {
         tph = tth + al4(2 * nt);             // float2 [np]
         rayq = tph + al4(2 * np_);           // uint [kRQ] ring
         owner = rayq + kRQ;                  // uint [64] round-stamped claims, indexed by pair slot
-        pdat = owner + 64;                   // [64][16] pair table: A[9], u0[3], w, rho, sigma, -
+        pdat = owner + 64;                   // pair table, 4 planes [4][64] float4: A[0:4] | A[4:8] | A[8], u0 | w, rho, sigma, -
         wave_stride = al4(pdat + 64 * 16);
         red = wave_base;                     // final reduction reuses the wave regions
         total = wave_base + kWaves * wave_stride;
@@ -992,9 +992,13 @@ struct BRay {
     float S0b, S1b, S2b, dsigb;          // netf: accumulators of part B (scaled by the ray's total at the end)
 };
 
-__device__ __forceinline__ void load_pdat(const float* pd, float* A, float* u0, float& w, float& rho, float& sigma) {
-    const float4* q4 = reinterpret_cast<const float4*>(pd);
-    const float4 a = q4[0], c = q4[1], e = q4[2], g = q4[3];
+// The pair table is stored as four planes of 64 float4 (plane c = float4 c of every pair slot): a lane's
+// ds_read_b128 of slot s starts at bank 4 (s mod 16), so the 16 lanes of a read group spread over the 16
+// bank quads (a [64][16] row layout started every row at one of 4 banks: up to 16-way conflicts)
+__device__ __forceinline__ void load_pdat(const float* pd, int slot, float* A, float* u0, float& w, float& rho,
+                                          float& sigma) {
+    const float4* q4 = reinterpret_cast<const float4*>(pd) + slot;
+    const float4 a = q4[0], c = q4[64], e = q4[128], g = q4[192];
     A[0] = a.x; A[1] = a.y; A[2] = a.z; A[3] = a.w; A[4] = c.x; A[5] = c.y; A[6] = c.z; A[7] = c.w; A[8] = e.x;
     u0[0] = e.y; u0[1] = e.z; u0[2] = e.w;
     w = g.x; rho = g.y; sigma = g.z;
@@ -1068,7 +1072,7 @@ template <int MODE, bool DENSE>
 __device__ __forceinline__ bool bray_setup(const float* pd, float2 th, float2 ph, int slot, int i, int j, int nr,
                                            float mc2, float r0, float dr, float inv_dr, float f0log2, BRay& b) {
     float A[9], u0[3], w, rho, sigma;
-    load_pdat(pd, A, u0, w, rho, sigma);
+    load_pdat(pd, slot, A, u0, w, rho, sigma);
     Ray R;
     if (!ray_setup<DENSE>(A, u0, th.x * ph.x, th.x * ph.y, th.y, mc2, r0, inv_dr, nr, R)) return false;
     b.pos = R.kl; b.kl = R.kl;
@@ -1200,11 +1204,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
             for (int t = 0; t < 6; ++t) M[t] = P.M[t];
             i0 = P.i0; i1 = P.i1; j0 = P.j0; j1 = P.j1;
             wpair = P.w;
-            float4* d4 = reinterpret_cast<float4*>(pdat + lane * 16);
+            float4* d4 = reinterpret_cast<float4*>(pdat) + lane;
             d4[0] = make_float4(P.A[0], P.A[1], P.A[2], P.A[3]);
-            d4[1] = make_float4(P.A[4], P.A[5], P.A[6], P.A[7]);
-            d4[2] = make_float4(P.A[8], P.u0[0], P.u0[1], P.u0[2]);
-            d4[3] = make_float4(P.w, P.rho, P.sigma, 0.f);
+            d4[64] = make_float4(P.A[4], P.A[5], P.A[6], P.A[7]);
+            d4[128] = make_float4(P.A[8], P.u0[0], P.u0[1], P.u0[2]);
+            d4[192] = make_float4(P.w, P.rho, P.sigma, 0.f);
         }
         // ray cache of the forward: cached pairs walk their recorded cells instead of enumerating
         unsigned long long cbits0 = 0ull, cbits1 = 0ull;
@@ -1257,7 +1261,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
                 if (take && !(k.opt.flags & 1)) {                  // flags 1: enumerate only
                     const unsigned e = rayq[(qhead + r) & (kRQ - 1)];
                     const int slot = e & 0xFF, i = (e >> 8) & 0xFFF, j = e >> 20;
-                    act = bray_setup<MODE, DENSE>(pdat + slot * 16, tth[i], tph[j], slot, i, j, nr, mc2, r0, dr,
+                    act = bray_setup<MODE, DENSE>(pdat, tth[i], tph[j], slot, i, j, nr, mc2, r0, dr,
                                                   inv_dr, f0log2, b) && !(k.opt.flags & 4);  // flags 4: no bins
                     if (MODE == NLOSGR_MODE_NETF && TAIL) b.T *= b.st;   // sin(theta) rides on T (BV rows)
                 }
@@ -1553,14 +1557,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
         // view-direction chain through rho (SH basis, d_features and its d_mu share) runs in
         // sh_kernel from the stored dL/drho, which keeps 16 feature accumulators out of this kernel
         if (MODE == NLOSGR_MODE_NOOCL && active) {
-            const float4 wrs = reinterpret_cast<const float4*>(pdat + lane * 16)[3];   // w, rho, sigma
+            const float4 wrs = reinterpret_cast<const float4*>(pdat)[192 + lane];   // w, rho, sigma
             dSig += s0_pair * wrs.y;
             drho_pair = s0_pair * wrs.z;
         }
         if (active && wpair > 0.f) {
             const float q[3] = {px - mu[0], py - mu[1], pz - mu[2]};
-            const float4* d4 = reinterpret_cast<const float4*>(pdat + lane * 16);
-            const float4 a = d4[0], c = d4[1], e = d4[2];
+            const float4* d4 = reinterpret_cast<const float4*>(pdat) + lane;
+            const float4 a = d4[0], c = d4[64], e = d4[128];
             const float A[9] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w, e.x};
             for (int r = 0; r < 3; ++r)
                 for (int cc = 0; cc < 3; ++cc) dA[3 * r + cc] += dU0p[r] * q[cc];
