@@ -930,9 +930,10 @@ __global__ __launch_bounds__(kBlock) void fwd_dense_kernel(KArgs k) {
 // Lane-serial backward drain: lane = one ray segment, kBSteps bins per round (the upstream
 // gradient reads of a round are issued together), sums S_n = sum H pdf kap^n in registers.  A
 // finished ray's closed-form result (dL/du0, dL/dv, dsigma, drho) is handed to the lane that owns
-// its pair: finished lanes claim owner[slot] with a round stamp, each pair lane gathers its
-// claimant's result with ds_bpermute and folds it into the Gaussian's register accumulators.
-// Losers keep their result and retry next round.  No LDS float atomics, no pair/row tables.
+// its pair: finished lanes claim their pair lane with a forward permute (the highest claimant of a
+// pair wins), each pair lane gathers its claimant's result with ds_bpermute and folds it into the
+// Gaussian's register accumulators.  Losers keep their result and retry next round.  No LDS float
+// atomics, no claim tables.
 #ifndef NLOSGR_BSTEPS
 #define NLOSGR_BSTEPS 24
 #endif
@@ -949,7 +950,7 @@ constexpr int kShPart = 28;     // sh_kernel partial: dF[KM <= 25], dMu[3] (at K
 // workgroup (staged by all 256 threads one wall point ahead, one barrier per wall point), so the
 // LDS no longer scales with 4 x nr (C5, nr = 2048: 56 KB -> 39 KB per workgroup, 2 -> 4 per CU).
 struct BwdLayout {
-    int wave_base, wave_stride, grow, tth, tph, rayq, owner, pdat, red, total, buf_stride;
+    int wave_base, wave_stride, grow, tth, tph, rayq, pdat, red, total, buf_stride;
     __host__ __device__ BwdLayout(int nr, int nt, int np_, bool shared = false) {
         buf_stride = 0;
         if (shared) {
@@ -959,8 +960,7 @@ struct BwdLayout {
             buf_stride = tph + al4(2 * np_);
             wave_base = 2 * buf_stride;
             rayq = 0;                                 // per-wave region (relative to the wave's base)
-            owner = rayq + kRQ;
-            pdat = owner + 64;
+            pdat = rayq + kRQ;
             wave_stride = al4(pdat + 64 * 16);
             red = 0;                                  // unused: waves own distinct Gaussians
             total = wave_base + kWaves * wave_stride;
@@ -971,8 +971,7 @@ struct BwdLayout {
         tth = al4(nr + kBSteps);             // float2 [nt]
         tph = tth + al4(2 * nt);             // float2 [np]
         rayq = tph + al4(2 * np_);           // uint [kRQ] ring
-        owner = rayq + kRQ;                  // uint [64] round-stamped claims, indexed by pair slot
-        pdat = owner + 64;                   // pair table, 4 planes [4][64] float4: A[0:4] | A[4:8] | A[8], u0 | w, rho, sigma, -
+        pdat = rayq + kRQ;                   // pair table, 4 planes [4][64] float4: A[0:4] | A[4:8] | A[8], u0 | w, rho, sigma, -
         wave_stride = al4(pdat + 64 * 16);
         red = wave_base;                     // final reduction reuses the wave regions
         total = wave_base + kWaves * wave_stride;
@@ -1113,7 +1112,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
     float2* tth = reinterpret_cast<float2*>(gbase + L.tth);
     float2* tph = reinterpret_cast<float2*>(gbase + L.tph);
     unsigned* rayq = reinterpret_cast<unsigned*>(wb + L.rayq);
-    unsigned* owner = reinterpret_cast<unsigned*>(wb + L.owner);
     float* pdat = wb + L.pdat;
 
     const int gb = k.g_lo + blockIdx.x * (shr ? kNB * kWaves : kNB);
@@ -1170,7 +1168,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
             for (int t = ln; t < np_; t += 64)
                 tph[t] = make_float2(k.geo.cos_phi[(size_t)p * np_ + t], k.geo.sin_phi[(size_t)p * np_ + t]);
         }
-        owner[lane] = 0xFFFFFFFFu;
         const float px = k.geo.wall[3 * p], py = k.geo.wall[3 * p + 1], pz = k.geo.wall[3 * p + 2];
         // per-pair row offset, recomputed per wall point (not hoisted as per-lane 64-bit pointers)
         int gio = gi;
@@ -1227,7 +1224,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
         const float* gray = RAYS && k.grad_ray ? k.grad_ray + (size_t)p * nt * np_ * nr : nullptr;
         wave_sync();
         int ci = i0, cj = j0, qhead = 0, qcount = 0;
-        unsigned round = 0;
         bool act = false, pend = false;
         float dU0p[3] = {0.f, 0.f, 0.f}, drho_pair = 0.f, s0_pair = 0.f;
         BRay b;
@@ -1519,15 +1515,22 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
             }
             const unsigned long long pmask = __builtin_amdgcn_ballot_w64(pend);
             if (pmask) {
-                // hand finished rays to their pair lanes: per pair and round one claimant (stamped
-                // claim in LDS), its result fetched by the pair lane with bpermute
-                const unsigned stamp = (round << 8) | (unsigned)lane;
-                if (pend) owner[b.slot] = stamp;
-                wave_sync();
-                const unsigned ow = owner[lane];
-                const bool got = (ow >> 8) == (round & 0xFFFFFFu);
-                const int src = got ? (int)(ow & 63u) : lane;
-                const bool won = pend && owner[b.slot] == stamp;
+                // hand finished rays to their pair lanes: per pair and round one claimant, its result
+                // fetched by the pair lane with bpermute.  The claim is a forward permute (ds_permute_b32,
+                // no LDS memory, no fences): every pending lane sends lane + 1 to its pair lane, and of
+                // several senders to one lane the highest lane's value arrives (lanes nobody writes
+                // receive 0; measured on gfx950, scripts/permute_probe.hip).  Every lane that must
+                // receive also sends, so the lanes without a result park a 0 on lane 0 in one permute and
+                // on lane 1 in a second; lane 0 reads the second, every other lane the first.
+                const int pv = pend ? lane + 1 : 0;
+                const int w1 = __builtin_amdgcn_ds_permute((pend ? b.slot : 0) << 2, pv);
+                const int w2 = __builtin_amdgcn_ds_permute((pend ? b.slot : 1) << 2, pv);
+                const int wcl = lane == 0 ? w2 : w1;
+                const bool got = wcl != 0;
+                const int src = got ? wcl - 1 : lane;
+                // (all lanes execute the bpermute: a source lane inactive in EXEC reads as 0)
+                const int wpair = __builtin_amdgcn_ds_bpermute(b.slot << 2, wcl);
+                const bool won = pend && wpair == lane + 1;
                 const float gm = got ? 1.f : 0.f;
                 float gU[3], gV[3];
                 // every lane must execute the bpermute: it cannot read lanes that are inactive in EXEC
@@ -1548,9 +1551,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
                     dSig += gSig;
                     drho_pair += gRho;
                 }
-                wave_sync();
                 if (won) pend = false;
-                ++round;
             }
         }
         // chain of this wall point's pair (Gaussian gi, wall point p) through u0 = A (p - mu); the

@@ -5,7 +5,7 @@ forward and backward of the no-occlusion volume, variants interleaved, median of
 
 Each positional argument is one variant (comma-separated NAME=VALUE pairs, '-' for none).  Prints one
 JSON line: per variant fwd/bwd medians and the forward's rel-L2 against the first variant."""
-import argparse, dataclasses, json, os, statistics, sys, time
+import argparse, dataclasses, hashlib, json, os, statistics, sys, time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, 'nlos-gaussian-renderer_amd')); sys.path.insert(0, ROOT)
 import torch
@@ -44,6 +44,7 @@ def unsetenv(v):
 
 
 grad = None
+hashes = {}
 res = {v: {'fwd': [], 'bwd': []} for v in a.variants}
 out = {}
 for rep in range(a.reps + 1):
@@ -59,9 +60,11 @@ for rep in range(a.reps + 1):
         tb = 0.0
         if a.bwd:
             t0 = time.perf_counter()
-            render_backward(*args, cfg, grad_hist=grad)
+            d = render_backward(*args, cfg, grad_hist=grad)
             torch.cuda.synchronize()
             tb = (time.perf_counter() - t0) * 1e3
+            if rep == 0:   # bitwise fingerprint of the gradients (compare across processes / libraries)
+                hashes[v] = hashlib.sha1(b"".join(x.detach().cpu().numpy().tobytes() for x in d)).hexdigest()[:16]
         unsetenv(v)
         if rep == 0:
             out[v] = hist
@@ -74,5 +77,6 @@ line = {'config': a.config, 'cutoff': a.cutoff, 'mode': a.mode, 'variants': {}}
 for v in a.variants:
     med = lambda x: statistics.median(x) if x else None
     line['variants'][v] = {'fwd_ms': med(res[v]['fwd']), 'bwd_ms': med(res[v]['bwd']),
-                           'rel_l2_vs_first': ((out[v] - ref).norm() / ref.norm()).item()}
+                           'rel_l2_vs_first': ((out[v] - ref).norm() / ref.norm()).item(),
+                           'grad_sha1': hashes.get(v)}
 print(json.dumps(line))
