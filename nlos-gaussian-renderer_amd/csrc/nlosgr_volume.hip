@@ -941,6 +941,11 @@ constexpr int kBSteps = NLOSGR_BSTEPS;   // bins per lane per backward drain rou
 #ifndef NLOSGR_BSTEPS_NETF
 #define NLOSGR_BSTEPS_NETF 16
 #endif
+#ifndef NLOSGR_BSTEPS_TAIL
+#define NLOSGR_BSTEPS_TAIL 32
+#endif
+// the staged gradient row is zero-padded by the longest round (no-occlusion TAIL rounds)
+constexpr int kBPad = NLOSGR_BSTEPS_TAIL > kBSteps ? NLOSGR_BSTEPS_TAIL : kBSteps;
 constexpr int kBwdSlots = 13;   // per-Gaussian backward partial: dA[9], dMu[3], dsigma (stride 32 in HBM)
 constexpr int kShPart = 28;     // sh_kernel partial: dF[KM <= 25], dMu[3] (at KM), pad
 
@@ -955,7 +960,7 @@ struct BwdLayout {
         buf_stride = 0;
         if (shared) {
             grow = 0;                                 // buffer b at smem + b * buf_stride
-            tth = al4(nr + kBSteps);
+            tth = al4(nr + kBPad);
             tph = tth + al4(2 * nt);
             buf_stride = tph + al4(2 * np_);
             wave_base = 2 * buf_stride;
@@ -967,8 +972,8 @@ struct BwdLayout {
             return;
         }
         wave_base = 0;
-        grow = 0;                            // [nr + kBSteps] upstream gradient x att x hscale, zero pad
-        tth = al4(nr + kBSteps);             // float2 [nt]
+        grow = 0;                            // [nr + kBPad] upstream gradient x att x hscale, zero pad
+        tth = al4(nr + kBPad);               // float2 [nt]
         tph = tth + al4(2 * nt);             // float2 [np]
         rayq = tph + al4(2 * np_);           // uint [kRQ] ring
         pdat = rayq + kRQ;                   // pair table, 4 planes [4][64] float4: A[0:4] | A[4:8] | A[8], u0 | w, rho, sigma, -
@@ -1003,7 +1008,7 @@ __device__ __forceinline__ void load_pdat(const float* pd, int slot, float* A, f
     w = g.x; rho = g.y; sigma = g.z;
 }
 
-// grow[k] = dL/dhist[p,k] att[k] hscale[p], zero-padded to nr + kBSteps.  Rows of nr % 4 == 0
+// grow[k] = dL/dhist[p,k] att[k] hscale[p], zero-padded to nr + kBPad.  Rows of nr % 4 == 0
 // are staged with 16-B loads issued together (one memory round trip per 1024 bins per lane).
 // lane index the compiler cannot hoist: per-wall-point staging addresses are recomputed (a few
 // VALU ops) instead of being kept live across the backward's wall-point loop (they spilled)
@@ -1038,7 +1043,7 @@ __device__ __forceinline__ void stage_grow(const float* grad, const float* att, 
     } else {
         for (int t = lane; t < nr; t += 64) grow[t] = grad ? grad[t] * att[t] * hs : 0.f;
     }
-    for (int t = nr + lane; t < nr + kBSteps; t += 64) grow[t] = 0.f;
+    for (int t = nr + lane; t < nr + kBPad; t += 64) grow[t] = 0.f;
 }
 
 // shared layout: the whole workgroup stages wall point p's row and tables into one buffer
@@ -1060,7 +1065,7 @@ __device__ __forceinline__ void stage_shared(const KArgs& k, int p, int nr, int 
     } else {
         for (int t = t0; t < nr; t += kBlock) grow[t] = grad ? grad[t] * att[t] * hs : 0.f;
     }
-    for (int t = nr + t0; t < nr + kBSteps; t += kBlock) grow[t] = 0.f;
+    for (int t = nr + t0; t < nr + kBPad; t += kBlock) grow[t] = 0.f;
     for (int t = t0; t < nt; t += kBlock)
         tth[t] = make_float2(k.geo.sin_theta[(size_t)p * nt + t], k.geo.cos_theta[(size_t)p * nt + t]);
     for (int t = t0; t < np_; t += kBlock)
@@ -1099,8 +1104,11 @@ __device__ __forceinline__ bool bray_setup(const float* pd, float2 th, float2 ph
 template <int PRESET, int MODE, bool DENSE, bool RAYS, bool CACHE, bool SHR, bool TAIL = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) void bwd_kernel(KArgs k) {
     // bins per drain round: netf keeps more per-ray state, so its rounds are shorter (no spill at 128 VGPRs)
-    constexpr int kRS = MODE == NLOSGR_MODE_NETF ? NLOSGR_BSTEPS_NETF : kBSteps;
-    static_assert(kRS <= kBSteps && kRS % 2 == 0, "the staged row is padded by kBSteps bins");
+    // (the no-occlusion TAIL rounds are longer: 32 bins measured 1137 vs 1170 ms at 24 on C3, and only
+    // that variant stays spill-free at 32)
+    constexpr int kRS = MODE == NLOSGR_MODE_NETF ? NLOSGR_BSTEPS_NETF
+                        : (MODE == NLOSGR_MODE_NOOCL && TAIL && !RAYS && !DENSE && !CACHE && !SHR) ? NLOSGR_BSTEPS_TAIL : kBSteps;
+    static_assert(kRS <= kBPad && kRS % 4 == 0, "the staged row is padded by kBPad bins; BV4 reads whole float4s");
     extern __shared__ __align__(16) float smem[];
     const int nr = k.geo.nr, nt = k.geo.nt, np_ = k.geo.np;
     constexpr bool shr = SHR;   // == (k.bshared != 0)
