@@ -62,7 +62,8 @@ constexpr int kCap = NLOSGR_MAX_PER_RAY;
 constexpr float kFullM2 = 180.0f;      // AABB selection: whole-ray support, pdf >= exp(-90)
 constexpr float kLog2e = 1.44269504088896341f;
 constexpr int kRowFloats = 32768;      // [ray][bin] float2 rows: 128 KB
-constexpr int kList = 32;              // live entries per wave list pass (8 floats each)
+constexpr int kList = 20;              // live entries per wave list pass (8 floats each)
+constexpr int kCullU = 2;              // cull: Gaussians per thread per round (one barrier pair per kCullU x threads)
 constexpr int kSlot = 6;               // backward pair slot: m0 m1 m2 dsigma drho | key
 
 struct TArgs {
@@ -102,7 +103,7 @@ struct TLayout {   // offsets in floats
         rows = 0;
         stage = rows + 2 * rt * nr;
         queue = stage + kWin * kStage;
-        misc = queue + tb + kWin;          // queue capacity: one cull round + one window
+        misc = queue + kCullU * tb + kWin;   // queue capacity: one cull round + one window
         comb = misc + 256;
         // shared scratch: backward combine [kWin][16] / (rays phase) per-wave entry lists
         // [waves][kList][8] / (backward pairs) per-wave pair slots [waves][64][kSlot]
@@ -224,8 +225,8 @@ __global__ __launch_bounds__(tile_threads<BWD>()) void tile_kernel(TArgs k) {
     float* misc = sm + L.misc;
     int* icnt = reinterpret_cast<int*>(misc);          // [64] AABB cap counters per ray
     int* ihalf = icnt + 64;                             // [64] per-window hits of the first staged half
-    int* iwave = icnt + 128;                            // [16] cull counts per wave
-    float* cone = misc + 144;                           // axis xyz, cos h, sin h, pass-all flag
+    int* iwave = icnt + 128;                            // [kCullU][16] cull counts per wave
+    float* cone = misc + 160;                           // axis xyz, cos h, sin h, pass-all flag
     const int tid = threadIdx.x, wave = tid >> 6, lane = lane_id();
     const int RT = k.rt;
     // AABB selection: each selected Gaussian over the samples within the cutoff (5.7 sigma = parity
@@ -317,36 +318,64 @@ __global__ __launch_bounds__(tile_threads<BWD>()) void tile_kernel(TArgs k) {
             }
             int qn = 0;
             bool capped = false;   // AABB: every ray of the tile holds its 256 selections (nothing later counts)
-            for (int g0 = 0; !skip0 && !capped && (g0 < k.g.ng || qn > 0); g0 += kTB) {
-                // ---- cull round: lane = Gaussian, 512 per round, ordered append ----
+            // the cull records of the next round are loaded one round ahead (their L2 round trip overlaps
+            // the current round's barriers and windows); kCullU blocks of kTB Gaussians per round
+            float4 cnext[kCullU];
+#pragma unroll
+            for (int u = 0; u < kCullU; ++u) {
+                cnext[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (!skip0 && u * kTB + tid < k.g.ng) cnext[u] = k.cull[u * kTB + tid];
+            }
+            for (int g0 = 0; !skip0 && !capped && (g0 < k.g.ng || qn > 0); g0 += kCullU * kTB) {
+                // ---- cull round: lane = Gaussian, kCullU x kTB per round, ordered append ----
                 if (g0 < k.g.ng) {
-                    const int gi = g0 + tid;
-                    bool hit = false;
-                    if (gi < k.g.ng) {
-                        const float4 c = k.cull[gi];
-                        const float vx = c.x - px, vy = c.y - py, vz = c.z - pz;
-                        const float d2 = vx * vx + vy * vy + vz * vz;
-                        const float R2 = c.w * c.w;
-                        if (pass_all || d2 <= R2 || !(c.w < INFINITY)) {
-                            hit = true;
-                        } else {
-                            // angle(v, axis) <= h + asin(R / |v|)  <=>  v.a >= cos h sqrt(|v|^2 - R^2) - sin h R
-                            hit = vx * ax + vy * ay + vz * az >= ch * sqrtf(d2 - R2) - shh * c.w;
+                    bool hit[kCullU];
+                    unsigned long long m[kCullU];
+#pragma unroll
+                    for (int u = 0; u < kCullU; ++u) {
+                        const int gi = g0 + u * kTB + tid;
+                        const float4 c = cnext[u];
+                        if (gi + kCullU * kTB < k.g.ng) cnext[u] = k.cull[gi + kCullU * kTB];
+                        hit[u] = false;
+                        if (gi < k.g.ng) {
+                            const float vx = c.x - px, vy = c.y - py, vz = c.z - pz;
+                            const float d2 = vx * vx + vy * vy + vz * vz;
+                            const float R2 = c.w * c.w;
+                            if (pass_all || d2 <= R2 || !(c.w < INFINITY)) {
+                                hit[u] = true;
+                            } else {
+                                // angle(v, axis) <= h + asin(R / |v|)  <=>  v.a >= cos h sqrt(|v|^2 - R^2) - sin h R
+                                hit[u] = vx * ax + vy * ay + vz * az >= ch * sqrtf(d2 - R2) - shh * c.w;
+                            }
                         }
+                        m[u] = __builtin_amdgcn_ballot_w64(hit[u]);
+                        if (lane == 0) iwave[u * kTW + wave] = __popcll(m[u]);
                     }
-                    const unsigned long long m = __builtin_amdgcn_ballot_w64(hit);
-                    if (lane == 0) iwave[wave] = __popcll(m);
                     __syncthreads();
-                    int base = qn;
-                    for (int w = 0; w < wave; ++w) base += iwave[w];
-                    if (hit) queue[base + lanes_below(m)] = gi;
-                    int tot = 0;
-                    for (int w = 0; w < kTW; ++w) tot += iwave[w];
-                    qn += tot;
+                    // the per-wave counts as int4 reads; block u's hits follow all of block u - 1's
+                    int run = qn;
+                    const int4* iw4 = reinterpret_cast<const int4*>(iwave);
+#pragma unroll
+                    for (int u = 0; u < kCullU; ++u) {
+                        int base = run, tot = 0;
+#pragma unroll
+                        for (int w4 = 0; w4 < kTW / 4; ++w4) {
+                            const int4 c4 = iw4[u * (kTW / 4) + w4];
+                            const int cw[4] = {c4.x, c4.y, c4.z, c4.w};
+#pragma unroll
+                            for (int v = 0; v < 4; ++v) {
+                                base += 4 * w4 + v < wave ? cw[v] : 0;
+                                tot += cw[v];
+                            }
+                        }
+                        if (hit[u]) queue[base + lanes_below(m[u])] = g0 + u * kTB + tid;
+                        run += tot;
+                    }
+                    qn = run;
                     __syncthreads();
                     TDIAG(tcull)
                 }
-                const bool last = g0 + kTB >= k.g.ng;
+                const bool last = g0 + kCullU * kTB >= k.g.ng;
                 // ---- windows of up to 128 staged Gaussians ----
                 while (qn >= kWin || (last && qn > 0)) {
                     const int nst = min(qn, kWin);
