@@ -787,14 +787,18 @@ __global__ __launch_bounds__(tile_threads<BWD>()) void tile_kernel(TArgs k) {
                         }
                     }
                     __syncthreads();
-                    // drop the staged window from the queue
+                    // drop the staged window from the queue (the rest can exceed one thread per entry:
+                    // a cull round appends up to kCullU x kTB, so it moves in passes of kTB; a pass
+                    // reads from nst + its range, past everything earlier passes wrote)
                     const int rest = qn - nst;
-                    int keep = 0;
-                    if (tid < rest) keep = queue[nst + tid];
-                    __syncthreads();
-                    if (tid < rest) queue[tid] = keep;
+                    for (int b0 = 0; b0 < rest; b0 += kTB) {
+                        int keep = 0;
+                        if (b0 + tid < rest) keep = queue[nst + b0 + tid];
+                        __syncthreads();
+                        if (b0 + tid < rest) queue[b0 + tid] = keep;
+                        __syncthreads();
+                    }
                     qn = rest;
-                    __syncthreads();
                     TDIAG(trays)
                     if (SEL == NLOSGR_SELECT_AABB) {
                         // the filter keeps the first 256 box hits by index per ray (ray_aabb.cu:10-61) and

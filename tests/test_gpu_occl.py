@@ -108,6 +108,19 @@ def test_occl_volume_vs_oracle(cutoff, deg):
     _grads_close(m, P, 3e-4, f"occl cutoff {cutoff}")
 
 
+def test_occl_dense_cull_round_overflows_one_block():
+    """2500 Gaussians at cutoff 0: every Gaussian of a cull round (2 blocks of threads) survives, so the
+    queue left after a staged window is longer than one thread per entry and moves in several passes."""
+    walls, box = _scene()
+    m = _model(2500, 0, 11, 0.6, -1.0)
+    g = torch.Generator().manual_seed(5)
+    gout = torch.randn(walls.shape[0], T, generator=g)
+    hist, _ = _hip(m, "occl", "support", 0.0, walls, box, gout)
+    P, ref, _ = _oracle(m, True, walls, box, gout=gout)
+    _close(hist, ref, 2e-4, msg="occl dense 2500")
+    _grads_close(m, P, 3e-4, "occl dense 2500")
+
+
 def test_occl_early_termination():
     """Dense, opaque Gaussians: T drops below 1e-4 inside the volume, so the reference's early exit
     (volume_renderer.cu:127-137) zeroes the tails; forward and gradients still match."""
