@@ -316,7 +316,7 @@ __global__ __launch_bounds__(tile_threads<BWD>()) void tile_kernel(TArgs k) {
                 for (int x = tid; x < RT * nr; x += kTB) rows[x] = src[x];
                 __syncthreads();
             }
-            int qn = 0;
+            int qn = 0, qh = 0;   // live queue entries: [qh, qn)
             bool capped = false;   // AABB: every ray of the tile holds its 256 selections (nothing later counts)
             // the cull records of the next round are loaded one round ahead (their L2 round trip overlaps
             // the current round's barriers and windows); kCullU blocks of kTB Gaussians per round
@@ -326,9 +326,19 @@ __global__ __launch_bounds__(tile_threads<BWD>()) void tile_kernel(TArgs k) {
                 cnext[u] = make_float4(0.f, 0.f, 0.f, 0.f);
                 if (!skip0 && u * kTB + tid < k.g.ng) cnext[u] = k.cull[u * kTB + tid];
             }
-            for (int g0 = 0; !skip0 && !capped && (g0 < k.g.ng || qn > 0); g0 += kCullU * kTB) {
+            for (int g0 = 0; !skip0 && !capped && (g0 < k.g.ng || qn > qh); g0 += kCullU * kTB) {
                 // ---- cull round: lane = Gaussian, kCullU x kTB per round, ordered append ----
                 if (g0 < k.g.ng) {
+                    if (qh > 0) {
+                        // what the windows left (< kWin entries) moves to the front once per cull round
+                        const int rest = qn - qh;
+                        int keep = 0;
+                        if (tid < rest) keep = queue[qh + tid];
+                        __syncthreads();
+                        if (tid < rest) queue[tid] = keep;
+                        qn = rest;
+                        qh = 0;
+                    }
                     bool hit[kCullU];
                     unsigned long long m[kCullU];
 #pragma unroll
@@ -377,10 +387,10 @@ __global__ __launch_bounds__(tile_threads<BWD>()) void tile_kernel(TArgs k) {
                 }
                 const bool last = g0 + kCullU * kTB >= k.g.ng;
                 // ---- windows of up to 128 staged Gaussians ----
-                while (qn >= kWin || (last && qn > 0)) {
-                    const int nst = min(qn, kWin);
+                while (qn - qh >= kWin || (last && qn > qh)) {
+                    const int nst = min(qn - qh, kWin);
                     if (tid < nst) {
-                        const int gi = queue[tid];
+                        const int gi = queue[qh + tid];
                         const GaussRec rec = k.recs[gi];
                         // the SH row is loaded with the record (its round trip overlaps the record's)
                         float fr[kMaxK];
@@ -723,7 +733,7 @@ __global__ __launch_bounds__(tile_threads<BWD>()) void tile_kernel(TArgs k) {
                             bool any = false;
                             for (int x = 0; x < 14; ++x) any |= cb[x] != 0.f;
                             if (any) {
-                                const int gi = queue[e];
+                                const int gi = queue[qh + e];
                                 // the slot row, the Gaussian's mean and its SH row are loaded up front so the
                                 // three memory round trips overlap (the row was read after the compute)
                                 float4* dst = reinterpret_cast<float4*>(k.acc + ((size_t)blockIdx.x * k.g.ng + gi) * kRec);
@@ -787,18 +797,7 @@ __global__ __launch_bounds__(tile_threads<BWD>()) void tile_kernel(TArgs k) {
                         }
                     }
                     __syncthreads();
-                    // drop the staged window from the queue (the rest can exceed one thread per entry:
-                    // a cull round appends up to kCullU x kTB, so it moves in passes of kTB; a pass
-                    // reads from nst + its range, past everything earlier passes wrote)
-                    const int rest = qn - nst;
-                    for (int b0 = 0; b0 < rest; b0 += kTB) {
-                        int keep = 0;
-                        if (b0 + tid < rest) keep = queue[nst + b0 + tid];
-                        __syncthreads();
-                        if (b0 + tid < rest) queue[b0 + tid] = keep;
-                        __syncthreads();
-                    }
-                    qn = rest;
+                    qh += nst;   // the staged window leaves the queue (the rest moves at the next cull round)
                     TDIAG(trays)
                     if (SEL == NLOSGR_SELECT_AABB) {
                         // the filter keeps the first 256 box hits by index per ray (ray_aabb.cu:10-61) and
@@ -810,7 +809,7 @@ __global__ __launch_bounds__(tile_threads<BWD>()) void tile_kernel(TArgs k) {
                         }
                         if (full) {
                             capped = true;
-                            qn = 0;
+                            qn = qh = 0;
                             break;
                         }
                     }
