@@ -22,12 +22,21 @@ strong scaling, value = 1 volume per step / max-over-ranks step time.  --replica
 every rank a full volume of its own capture (weak scaling).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config C3] [--cutoff 5.7] [--lines 3.0] [--band 8] [--replicas]
+
+Launch: under a launcher (torch.distributed.run: WORLD_SIZE set) every process is one rank and
+WORLD_SIZE must equal --gpus.  Without one, `--gpus N` > 1 starts N fresh child interpreters of this
+script itself (rank r -> GPU r, RCCL over xGMI, rendezvous on 127.0.0.1) BEFORE anything touches the
+GPU, waits for them and exits with the worst exit code; rank 0's line is the job's line.
+NLOSGR_BENCH_STUB=1 replaces the render step by a small CPU step (gloo) so the launcher, the barriers
+and the max-over-ranks timing can be rehearsed without a GPU (tests/test_bench_launch_cpu.py).
 """
 import argparse
 from dataclasses import replace
 import json
 import os
+import socket
 import statistics
+import subprocess
 import sys
 import time
 
@@ -165,35 +174,135 @@ class Snapshot:
         tr.adam.step_count, tr.iteration = self.count, self.iteration
 
 
+def _sync(dev):
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+
+
 def timed_run(step, steps, warmup, world, dev):
     """W untimed steps, then EXACTLY K steps between barrier + synchronize on both sides; returns
-    the max-over-ranks wall time and each step's (fwd_ms, bwd_ms) from its HIP events (step()
-    returns a callable read after the per-step synchronize, which the driver's contract keeps
-    inside the timed region)."""
+    the max-over-ranks wall time, this rank's own wall time and each step's (fwd_ms, bwd_ms) from
+    its HIP events (step() returns a callable read after the per-step synchronize, which the
+    driver's contract keeps inside the timed region)."""
     for _ in range(warmup):
         step()
-    torch.cuda.synchronize(dev)
+    _sync(dev)
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize(dev)
+    _sync(dev)
     t0 = time.perf_counter()
     phases = []
     for i in range(steps):
         phase = step()
-        torch.cuda.synchronize(dev)
+        _sync(dev)
         phases.append(phase())
         if PROGRESS:
             print(f"[bench] step {i + 1}/{steps} fwd {phases[-1][0]:.1f} ms bwd {phases[-1][1]:.1f} ms",
                   file=sys.stderr, flush=True)
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t0
+    _sync(dev)
+    own = elapsed = time.perf_counter() - t0
     if world > 1:
         t = torch.tensor([elapsed], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
-    return elapsed, phases
+    return elapsed, own, phases
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n, argv):
+    """`--gpus N` without a launcher: N fresh interpreters of this script, rank r on GPU r (the
+    torch.distributed.run environment: RANK, LOCAL_RANK, WORLD_SIZE, MASTER_ADDR=127.0.0.1,
+    MASTER_PORT).  Called before anything initialises the GPU, so the parent never holds a device
+    context.  If a rank fails the others are ended (they would wait at a barrier forever); the exit
+    code is the worst rank's."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    codes = [None] * n
+    while any(c is None for c in codes):
+        for i, p in enumerate(procs):
+            if codes[i] is None:
+                codes[i] = p.poll()
+        if any(c not in (None, 0) for c in codes):
+            for i, p in enumerate(procs):
+                if codes[i] is None:
+                    p.terminate()
+            for i, p in enumerate(procs):
+                if codes[i] is None:
+                    try:
+                        codes[i] = p.wait(timeout=30)
+                    except subprocess.TimeoutExpired:
+                        p.kill()
+                        codes[i] = p.wait()
+            break
+        time.sleep(0.2)
+    bad = [c for c in codes if c != 0]
+    if bad:
+        print(f"[bench] rank exit codes {codes}", file=sys.stderr, flush=True)
+        return max((abs(c) for c in bad), default=1) or 1
+    return 0
+
+
+def stub_main(a, world, rank):
+    """NLOSGR_BENCH_STUB=1: the launcher / barrier / timing path with a small CPU step (a
+    [256,256] matmul per step + an all-reduce of a 64-float 'gradient', gloo) in place of the
+    render.  Not a measurement: rehearses the contract without a GPU."""
+    dev = torch.device("cpu")
+    if world > 1:
+        dist.init_process_group(os.environ.get("NLOSGR_DIST_BACKEND", "gloo"))
+    if os.environ.get("NLOSGR_BENCH_STUB_FAIL_RANK") == str(rank):
+        raise SystemExit(3)        # launcher test: a rank that dies after the rendezvous
+    x = torch.randn(256, 256, generator=torch.Generator().manual_seed(rank))
+    grad = torch.zeros(64)
+
+    def step():
+        t0 = time.perf_counter()
+        y = x @ x
+        grad.fill_(float(y[0, 0]))
+        if world > 1:
+            dist.all_reduce(grad)
+        ms = (time.perf_counter() - t0) * 1e3
+        return lambda: (ms, 0.0)
+
+    elapsed, own, phases = timed_run(step, a.steps, a.warmup, world, dev)
+    ranks = _gather_ranks(world, rank, own, phases, "cpu")
+    if rank == 0:
+        print(json.dumps({"metric": "stub (launcher rehearsal)", "value": world * 1000.0 * a.steps / (elapsed * 1e3),
+                          "unit": "steps/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+                          "ms_per_step": elapsed * 1e3 / a.steps, "ranks": ranks,
+                          "dist": _dist_info(world)}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def _dist_info(world):
+    if world == 1 or not dist.is_initialized():
+        return {"backend": None, "world_size": 1}
+    return {"backend": str(dist.get_backend()), "world_size": dist.get_world_size()}
+
+
+def _gather_ranks(world, rank, own, phases, device):
+    """Every rank's own timed wall time and mean phase times, gathered on rank 0."""
+    mine = {"rank": rank, "device": device, "ms_per_step": own * 1e3 / max(1, len(phases)),
+            "fwd_ms": statistics.fmean(p[0] for p in phases) if phases else 0.0,
+            "bwd_ms": statistics.fmean(p[1] for p in phases) if phases else 0.0}
+    if world == 1:
+        return [mine]
+    allr = [None] * world
+    dist.all_gather_object(allr, mine)
+    return allr
 
 
 def main():
@@ -221,9 +330,20 @@ def main():
                     help="with N ranks: every rank renders a full volume of its own capture (weak scaling)")
     a = ap.parse_args()
 
+    if a.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        # no launcher: start the N ranks ourselves, before any torch.cuda call in this process
+        sys.exit(launch_ranks(a.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        print(f"[bench] WORLD_SIZE={world} but --gpus {a.gpus}: refusing to report a {world}-rank run "
+              f"as {a.gpus} GPUs", file=sys.stderr, flush=True)
+        sys.exit(2)
+    if os.environ.get("NLOSGR_BENCH_STUB") == "1":
+        return stub_main(a, world, rank)
     # NLOSGR_DIST_BACKEND=gloo rehearses N ranks on fewer GPUs (rank -> GPU local % count); the
     # production path is RCCL ("nccl"), one GPU per rank
     ndev = max(1, torch.cuda.device_count())
@@ -285,7 +405,7 @@ def main():
                 train()
                 return train.phase_ms   # HIP events of the step's phases (occl: summed over its batches)
 
-            elapsed, evs = timed_run(step, a.steps, a.warmup, world, dev)
+            elapsed, own, evs = timed_run(step, a.steps, a.warmup, world, dev)
             fwd_ms = [e[0] for e in evs]
             bwd_ms = [e[1] for e in evs] if not fwd_only else []
             snap.restore()
@@ -298,7 +418,7 @@ def main():
             per_band.append({"band": [b0, b1], "ms_per_step": elapsed * 1000.0 / a.steps,
                              "fwd_ms": statistics.fmean(fwd_ms), "bwd_ms": statistics.fmean(bwd_ms) if bwd_ms else 0.0,
                              "fwd_ms_all": fwd_ms, "bwd_ms_all": bwd_ms, "pairs": pairs, "rays": rays,
-                             "evaluations": evals, "nwall": int(idx.numel())})
+                             "evaluations": evals, "nwall": int(idx.numel()), "own_s": own, "phases": evs})
             del train, snap
             torch.cuda.empty_cache()
         results[cut] = per_band
@@ -371,6 +491,9 @@ def main():
                      "algorithmic_bytes_per_launch": dom_bytes, "avg_launch_ms": dom_ms},
         "compute": valu,
     }
+    if world > 1:
+        out["ranks"] = _gather_ranks(world, rank, main_bands[0]["own_s"], main_bands[0]["phases"], str(dev))
+        out["dist"] = _dist_info(world)
     if a.band > 1:
         out["bands"] = [{k: b[k] for k in ("band", "ms_per_step", "fwd_ms", "bwd_ms", "evaluations")}
                         for b in main_bands]
