@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define NLOSGR_ABI_VERSION 5
+#define NLOSGR_ABI_VERSION 6
 
 /* convention presets */
 enum {
@@ -135,6 +135,13 @@ typedef struct {
  * nwall * tiles * tile rays * nr * 8 B). */
 NLOSGR_API size_t nlosgr_workspace_bytes(const nlosgr_gaussians* g, const nlosgr_geometry* geo,
                               const nlosgr_options* opt);
+
+/* Batch budgets in MiB (values <= 0 keep the current one): the backward's dL/drho buffer, filled in
+ * wall-point batches (default 1024 or NLOSGR_DRHO_MB), and the ray-tile forward's partial histograms
+ * (default 1024 or NLOSGR_TILE_HPART_MB); both environment variables are read once, at first use.
+ * They set the workspace layout: change them only while no workspace sized under the old values is
+ * still in use (a ray-cache backward must run under the forward's budgets). */
+NLOSGR_API void nlosgr_set_batch_budgets(double drho_mb, double tile_hpart_mb);
 
 /* Forward.  hist_out [P,nr] (may be NULL):  hscale[p]*att[k]*sum_{g,i,j} w_g(p) sin(theta_i) pdf
  *           ray_out  [P,nt*np,nr] (may be NULL, caller zero-fills): ray_scale*sum_g w_g(p) pdf,

@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "nlosgr_device.hpp"
@@ -55,6 +56,25 @@ __device__ __forceinline__ float fsqrt(float x) { return __builtin_amdgcn_sqrtf(
 __device__ __forceinline__ float flog2(float x) { return __builtin_amdgcn_logf(x); }
 
 inline size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
+
+// Batch budgets that shape the workspace layout (MiB): the backward's dL/drho wall-point batches and
+// the ray-tile forward's partial histograms.  Defaults come from NLOSGR_DRHO_MB / NLOSGR_TILE_HPART_MB
+// read ONCE (first use); later changes go through nlosgr_set_batch_budgets only, so a workspace sized
+// by nlosgr_workspace_bytes and a ray-cache backward see the layout of the forward that filled it.
+struct BatchBudgets {
+    double drho_mb, tile_hpart_mb;
+};
+inline BatchBudgets& batch_budgets() {
+    static BatchBudgets b = [] {
+        BatchBudgets v;
+        const char* d = getenv("NLOSGR_DRHO_MB");
+        const char* h = getenv("NLOSGR_TILE_HPART_MB");
+        v.drho_mb = (d && atof(d) > 0.0) ? atof(d) : 1024.0;
+        v.tile_hpart_mb = (h && atof(h) > 0.0) ? atof(h) : 1024.0;
+        return v;
+    }();
+    return b;
+}
 
 #define HIPCHK(x)                                                                  \
     do {                                                                           \

@@ -932,7 +932,6 @@ __global__ __launch_bounds__(256) void tiles_finish_kernel(TArgs k, float* d_mu,
     chain_to_raw<NLOSGR_PRESET_CUDA>(k.g, i, a, d_scaling, d_rot);
 }
 
-constexpr size_t kHpartBytes = (size_t)1 << 30;   // forward tile partials per launch (1 GiB)
 
 int cu_count() {
     static int n = 0;
@@ -976,8 +975,7 @@ TPlan plan(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_o
     // forward tile partials per launch: at most kHpartBytes (C5 with AABB selection: 65536 wall points x
     // 128 tiles x 2048 bins would be 69 GB for the whole wall), so the forward runs in wall-point batches
     const size_t per_wall = (size_t)P.ntiles * geo->nr * sizeof(float);
-    const char* hm = getenv("NLOSGR_TILE_HPART_MB");   // override (tests: force wall-point batches)
-    const size_t budget = hm ? (size_t)(atof(hm) * 1048576.0) : kHpartBytes;
+    const size_t budget = (size_t)(batch_budgets().tile_hpart_mb * 1048576.0);   // default 1 GiB
     long long pb = per_wall ? (long long)(budget / per_wall) : geo->nwall;
     if (pb < 1) pb = 1;
     P.pbatch = (int)(pb < geo->nwall ? pb : geo->nwall);

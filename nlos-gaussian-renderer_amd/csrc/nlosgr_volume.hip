@@ -802,6 +802,457 @@ __global__ __launch_bounds__(kBlock) void hist_reduce_kernel(const float* __rest
     hist[i] = s * att[t] * hscale[p];
 }
 
+// ------------------------------------------------------------------------------------------
+// forward, window sweep (no-occlusion histogram at cutoff >= kTailCutoff: the training hot path)
+// ------------------------------------------------------------------------------------------
+// The lane-serial drain above is bound by the LDS array: every (segment, bin) value is one LDS
+// read-add-write at a random start bin (bank conflicts, claim losers).  Here the 64 lanes of a wave
+// walk the SAME 16-bin window [W, W+16) at a time, each on its own segment: lane l holds the values
+// of bins W..W+15 of its segment in 16 registers (exp2 seed at W, then the two-multiply recurrence),
+// and one reduce-scatter across the wave (permlane32/16 swaps, then DPP row_ror:8 / row_half_mirror /
+// quad_perm adds: 35 VALU for 1024 lane-bins) leaves every quad of lanes holding one bin's sum, which
+// one lane adds into the wave's LDS histogram: 16 conflict-free read-add-writes per window instead
+// of 1024.  For the lanes to share windows, the segments are collected in an LDS batch (records
+// ga, al, ks, kl|kh) and counting-sorted by start window ("bucket" = kl / 16); the sweep walks the
+// buckets upwards and free lanes take records of the current bucket (seeded at W <= kl: the bins
+// [W, kl) get the Gaussian's exact values outside the cutoff, as the TAIL drains' overrun past kh).
+// A free lane that finds the bucket empty takes the remainder [W, kh] of a record of the two buckets
+// behind (a "late" record); its head [kl, W - 1] ends on a window boundary and is swept in a later
+// pass, so no piece ever runs past a split point.  Lanes whose seed at W would underflow (Gaussians
+// much narrower than a bin, W < kl) take an exact per-bin exp2 path for that window.  The forward's
+// summation order is fixed by the sort and the lane order: deterministic.
+constexpr int kSW = 16;                    // bins per window (value registers per lane)
+#ifndef NLOSGR_SWEEP_CAP
+#define NLOSGR_SWEEP_CAP 640
+#endif
+constexpr int kSCap = NLOSGR_SWEEP_CAP;     // segment records per wave batch (<= 65535)
+constexpr float kSeedMin = -120.f;          // log2 of the smallest seed the recurrence starts from
+#ifndef NLOSGR_SWEEP_LATE
+#define NLOSGR_SWEEP_LATE 2
+#endif
+constexpr int kSLate = NLOSGR_SWEEP_LATE;   // windows behind W a free lane takes late remainders from
+
+struct SweepLayout {
+    int hist, ring, rec, idx, hidx, cnt, bcur, bend, wave_stride, total, nb;   // offsets in floats
+    __host__ __device__ SweepLayout(int nr, int nt, int np_) {
+        const int off = al4(2 * (nt + np_));
+        nb = (nr + kSW - 1) / kSW;
+        hist = 0;                               // [nb * kSW + kSW]: windows past nr land in the pad
+        ring = al4(nb * kSW + kSW);             // u32 [kRQ] candidate ray ring
+        rec = ring + kRQ;                       // float4 [kSCap] segment records
+        idx = rec + 4 * kSCap;                  // u16 [kSCap] bucket-sorted record ids
+        hidx = idx + al4((kSCap + 1) / 2);      // u16 [kSCap] heads left by late takes (next pass)
+        cnt = hidx + al4((kSCap + 1) / 2);      // int [nb] counting-sort cursors
+        bcur = cnt + al4(nb);                   // int [nb] next unread sorted position per bucket
+        bend = bcur + al4(nb);                  // int [nb] end of the bucket
+        wave_stride = al4(bend + nb);
+        hist += off; ring += off; rec += off; idx += off; hidx += off; cnt += off; bcur += off; bend += off;
+        total = off + kWaves * wave_stride;
+    }
+};
+
+__device__ __forceinline__ int rec_kl(float4 r) { return __float_as_int(r.w) & 0xFFFF; }
+__device__ __forceinline__ int rec_kh(float4 r) { return (int)((unsigned)__float_as_int(r.w) >> 16); }
+__device__ __forceinline__ float rec_pack(int kl, int kh) { return __int_as_float(kl | (kh << 16)); }
+
+template <int CTRL>
+__device__ __forceinline__ float dppf(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+
+// x[r] = this lane's value of bin W + r  ->  every lane returns the wave's sum for bin W + (lane >> 2)
+__device__ __forceinline__ float window_reduce(float* x) {
+    const int lane = lane_id();
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {   // lanes 32-63 of x[j] <-> lanes 0-31 of x[j+8]: bin j + 8 (lane >> 5)
+        const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x[j]), __float_as_uint(x[j + 8]), false, false);
+        x[j] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {   // odd rows of x[j] <-> even rows of x[j+4]: + 4 ((lane >> 4) & 1)
+        const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x[j]), __float_as_uint(x[j + 4]), false, false);
+        x[j] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+    }
+    const bool b3 = (lane & 8) != 0, b2 = (lane & 4) != 0;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {   // lane ^ 8 (row_ror:8): + 2 ((lane >> 3) & 1)
+        const float snd = b3 ? x[j] : x[j + 2], kp = b3 ? x[j + 2] : x[j];
+        x[j] = kp + dppf<0x128>(snd);
+    }
+    float s;
+    {   // lane <-> 7 - lane within 8 (row_half_mirror): + ((lane >> 2) & 1)
+        const float snd = b2 ? x[0] : x[1], kp = b2 ? x[1] : x[0];
+        s = kp + dppf<0x141>(snd);
+    }
+    s += dppf<0xB1>(s);   // quad_perm [1,0,3,2]
+    s += dppf<0x4E>(s);   // quad_perm [2,3,0,1]
+    return s;
+}
+
+// first bucket >= from with unread records, or -1 (wave-uniform)
+__device__ __forceinline__ int next_pending(const int* bcur, const int* bend, int nb, int from) {
+    for (int b0 = from; b0 < nb; b0 += 64) {
+        const int b = b0 + lane_id();
+        const unsigned long long m = __builtin_amdgcn_ballot_w64(b < nb && bcur[b] < bend[b]);
+        if (m) return b0 + (int)__builtin_ctzll(m);
+    }
+    return -1;
+}
+
+// counting sort of the records list[0..n) (nullptr: ids 0..n-1) by bucket into idx, bucket ranges
+// [bcur, bend).  LDS atomics return in lane order within an instruction: the order is deterministic.
+__device__ void sweep_sort(const float4* rec, const unsigned short* list, int n, unsigned short* idx, int* cnt,
+                           int* bcur, int* bend, int nb) {
+    const int lane = lane_id();
+    for (int b = lane; b < nb; b += 64) cnt[b] = 0;
+    wave_sync();
+    for (int i = lane; i < n; i += 64) {
+        const int id = list ? list[i] : i;
+        atomicAdd(&cnt[rec_kl(rec[id]) / kSW], 1);
+    }
+    wave_sync();
+    const int per = (nb + 63) / 64;
+    int s = 0;
+    for (int u = 0; u < per; ++u) {
+        const int b = lane * per + u;
+        if (b < nb) s += cnt[b];
+    }
+    int incl = s;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(incl, o);
+        if (lane >= o) incl += y;
+    }
+    int run = incl - s;
+    for (int u = 0; u < per; ++u) {
+        const int b = lane * per + u;
+        if (b < nb) {
+            const int c = cnt[b];
+            bcur[b] = run;
+            bend[b] = run + c;
+            cnt[b] = run;
+            run += c;
+        }
+    }
+    wave_sync();
+    for (int i = lane; i < n; i += 64) {
+        const int id = list ? list[i] : i;
+        const int pos = atomicAdd(&cnt[rec_kl(rec[id]) / kSW], 1);
+        idx[pos] = (unsigned short)id;
+    }
+    wave_sync();
+}
+
+// sweep the batch rec[0..n) into the wave's histogram (see above); leaves the batch empty
+#ifdef NLOSGR_SWEEP_DEBUG
+#define NLOSGR_DBG_ARG , long long& dbg_got, long long& dbg_win, long long& dbg_pass
+#define NLOSGR_DBG_PASS , dbg_got, dbg_win, dbg_pass
+#else
+#define NLOSGR_DBG_ARG
+#define NLOSGR_DBG_PASS
+#endif
+// Refill, issued one window ahead (its LDS reads overlap the window being computed): lanes free at
+// window Wn (fr) are assigned records of Wn's bucket, then of the kSLate buckets behind (late);
+// the bucket cursors advance now, the records land in (pid, pr) for sweep_commit.
+struct SweepPf {
+    bool pf, late;
+    int pid;
+    float4 pr;
+};
+__device__ __forceinline__ void sweep_issue(int Wn, bool fr, const float4* rec, const unsigned short* idx, int* bcur,
+                                            const int* bend, int nb, SweepPf& f) {
+    const int lane = lane_id();
+    f.pf = false; f.late = false; f.pid = 0;
+    const unsigned long long fm = __builtin_amdgcn_ballot_w64(fr);
+    const int nfree = __popcll(fm);
+    if (nfree == 0) return;
+    const int rank = lanes_below(fm);
+    const int bb = Wn / kSW;
+    int took = 0;
+    if (bb < nb) {
+        const int c0 = __builtin_amdgcn_readfirstlane(bcur[bb]);
+        const int c1 = __builtin_amdgcn_readfirstlane(bend[bb]);
+        const int k1 = min(nfree, c1 - c0);
+        if (k1 > 0) {
+            if (fr && rank < k1) { f.pid = idx[c0 + rank]; f.pf = true; }
+            if (lane == 0) bcur[bb] = c0 + k1;
+            took = k1;
+        }
+    }
+#pragma unroll
+    for (int back = 1; back <= kSLate; ++back) {
+        const int lb = bb - back;
+        if (took >= nfree || lb < 0) break;
+        if (lb >= nb) continue;
+        const int c0 = __builtin_amdgcn_readfirstlane(bcur[lb]);
+        const int c1 = __builtin_amdgcn_readfirstlane(bend[lb]);
+        const int k2 = min(nfree - took, c1 - c0);
+        if (k2 <= 0) continue;
+        if (fr && rank >= took && rank < took + k2) { f.pid = idx[c0 + rank - took]; f.pf = true; f.late = true; }
+        if (lane == 0) bcur[lb] = c0 + k2;
+        took += k2;
+    }
+    if (f.pf) f.pr = rec[f.pid];
+}
+
+// lane state of the sweep: the segment (ga, al, ks) on [kl, kh] and cc = 2^(2 ga)
+struct SweepLane {
+    bool busy;
+    float ga, al, ks, cc;
+    int kl, kh;
+    __device__ __forceinline__ void idle() { busy = false; ga = 0.f; al = -1000.f; ks = 0.f; cc = 1.f; kl = 0; kh = -1; }
+};
+
+// apply an issued refill at window Wn: eligible records start here (seeded at Wn <= kl); a late record
+// gives its remainder [Wn, kh] when that is at least a window long and leaves its head [kl, Wn - 1]
+// (or, when shorter, the whole record) for the next pass
+__device__ __forceinline__ void sweep_commit(int Wn, const SweepPf& f, float4* rec, unsigned short* hidx, int& nheads,
+                                             SweepLane& L) {
+    bool head = false;
+    if (f.pf) {
+        const int rkl = rec_kl(f.pr), rkh = rec_kh(f.pr);
+        if (!f.late || rkh >= Wn + kSW - 1) {
+            L.busy = true;
+            L.ga = f.pr.x; L.al = f.pr.y; L.ks = f.pr.z;
+            L.kl = f.late ? Wn : rkl;
+            L.kh = rkh;
+            L.cc = fast_exp2(2.f * L.ga);
+            if (f.late) rec[f.pid].w = rec_pack(rkl, Wn - 1);
+        }
+        head = f.late;
+    }
+    const unsigned long long hm = __builtin_amdgcn_ballot_w64(head);
+    if (head) hidx[nheads + lanes_below(hm)] = (unsigned short)f.pid;
+    nheads += __popcll(hm);
+    if (!L.busy) L.idle();
+}
+
+// sweep the batch rec[0..n) into the wave's histogram (see above); leaves the batch empty
+#ifdef NLOSGR_SWEEP_DEBUG
+#define NLOSGR_DBG_ARG , long long& dbg_got, long long& dbg_win, long long& dbg_pass
+#define NLOSGR_DBG_PASS , dbg_got, dbg_win, dbg_pass
+#else
+#define NLOSGR_DBG_ARG
+#define NLOSGR_DBG_PASS
+#endif
+__device__ void sweep_batch(float4* rec, unsigned short* idx, unsigned short* hidx, int* cnt, int* bcur, int* bend,
+                            float* hist, int n, int nb NLOSGR_DBG_ARG) {
+    const int lane = lane_id();
+    int nlist = n;
+    bool first = true;
+    while (nlist > 0) {
+        sweep_sort(rec, first ? nullptr : hidx, nlist, idx, cnt, bcur, bend, nb);
+        first = false;
+#ifdef NLOSGR_SWEEP_DEBUG
+        if (lane == 0) dbg_pass += 1;
+#endif
+        int nheads = 0;
+        SweepLane L;
+        L.idle();
+        SweepPf f;
+        int W = next_pending(bcur, bend, nb, 0) * kSW;
+        sweep_issue(W, true, rec, idx, bcur, bend, nb, f);
+        sweep_commit(W, f, rec, hidx, nheads, L);
+        while (true) {
+            if (!__builtin_amdgcn_ballot_w64(L.busy)) {   // every lane idle: jump to the next pending window
+                int nb2 = next_pending(bcur, bend, nb, W / kSW + 1);
+                if (nb2 < 0) nb2 = next_pending(bcur, bend, nb, 0);
+                if (nb2 < 0) break;
+                W = nb2 * kSW;
+                sweep_issue(W, true, rec, idx, bcur, bend, nb, f);
+                sweep_commit(W, f, rec, hidx, nheads, L);
+                continue;
+            }
+            // refill of the next window, issued now
+            sweep_issue(W + kSW, !(L.busy && L.kh >= W + kSW), rec, idx, bcur, bend, nb, f);
+            // the window: two exp2 seeds (W, W + 8), then value(t+1) = value(t) q, q *= cc on each half
+            const float ta = (float)W - L.ks, tb = ta + (float)(kSW / 2);
+            const float ea = fmaf(L.ga, ta * ta, L.al), eb = fmaf(L.ga, tb * tb, L.al);
+            float ca = fast_exp2(ea), qa = fast_exp2(L.ga * fmaf(2.f, ta, 1.f));
+            float cb = fast_exp2(eb), qb = fast_exp2(L.ga * fmaf(2.f, tb, 1.f));
+            float x[kSW];
+            const bool exact = L.busy && (ea < kSeedMin || eb < kSeedMin);
+            if (__builtin_amdgcn_ballot_w64(exact)) {
+                // a seed that would underflow (narrow Gaussian, W < kl): exact values of [kl, kh]
+#pragma unroll
+                for (int r = 0; r < kSW; ++r) {
+                    const float tr = ta + (float)r;
+                    const int bin = W + r;
+                    const float ve = (bin >= L.kl && bin <= L.kh) ? fast_exp2(fmaf(L.ga, tr * tr, L.al)) : 0.f;
+                    const float vr = r < kSW / 2 ? ca : cb;
+                    x[r] = exact ? ve : vr;
+                    if (r < kSW / 2) { ca *= qa; qa *= L.cc; } else { cb *= qb; qb *= L.cc; }
+                }
+            } else {
+#pragma unroll
+                for (int r = 0; r < kSW / 2; ++r) {
+                    x[r] = ca;
+                    x[r + kSW / 2] = cb;
+                    ca *= qa;
+                    cb *= qb;
+                    qa *= L.cc;
+                    qb *= L.cc;
+                }
+            }
+#ifdef NLOSGR_SWEEP_DEBUG
+            if (L.busy) {
+                const int lo = max(W, L.kl), hi = min(W + kSW - 1, L.kh);
+                if (hi >= lo) dbg_got += hi - lo + 1;
+            }
+            if (lane == 0) dbg_win += 1;
+#endif
+            const float s = window_reduce(x);
+            if ((lane & 3) == 0) {
+                float* h = hist + W + (lane >> 2);
+                *h += s;
+            }
+            W += kSW;
+            if (!(L.busy && L.kh >= W)) L.idle();
+            sweep_commit(W, f, rec, hidx, nheads, L);
+        }
+        wave_sync();
+        nlist = nheads;
+    }
+}
+
+template <int PRESET>
+__global__ __launch_bounds__(kBlock) void fwd_sweep_kernel(KArgs k) {
+    extern __shared__ __align__(16) float smem[];
+    const int nr = k.geo.nr, nt = k.geo.nt, np_ = k.geo.np;
+    const SweepLayout L(nr, nt, np_);
+    float2* tth = reinterpret_cast<float2*>(smem);
+    float2* tph = tth + nt;
+    const int wave = threadIdx.x >> 6, lane = lane_id();
+    float* wb = smem + wave * L.wave_stride;
+    float* hist = wb + L.hist;
+    unsigned* rayq = reinterpret_cast<unsigned*>(wb + L.ring);
+    float4* rec = reinterpret_cast<float4*>(wb + L.rec);
+    unsigned short* idx = reinterpret_cast<unsigned short*>(wb + L.idx);
+    unsigned short* hidx = reinterpret_cast<unsigned short*>(wb + L.hidx);
+    int* cnt = reinterpret_cast<int*>(wb + L.cnt);
+    int* bcur = reinterpret_cast<int*>(wb + L.bcur);
+    int* bend = reinterpret_cast<int*>(wb + L.bend);
+    const int nb = L.nb;
+    const int p = blockIdx.x;
+    const int gsplit = blockIdx.y, nsp = gridDim.y;
+    const int gper = (((k.g.ng + nsp - 1) / nsp) + 63) & ~63;
+    const int g_lo = gsplit * gper, g_hi = min(k.g.ng, g_lo + gper);
+
+    for (int t = threadIdx.x; t < nt; t += blockDim.x)
+        tth[t] = make_float2(k.geo.sin_theta[(size_t)p * nt + t], k.geo.cos_theta[(size_t)p * nt + t]);
+    for (int t = threadIdx.x; t < np_; t += blockDim.x)
+        tph[t] = make_float2(k.geo.cos_phi[(size_t)p * np_ + t], k.geo.sin_phi[(size_t)p * np_ + t]);
+    for (int t = lane; t < nb * kSW + kSW; t += 64) hist[t] = 0.f;
+    __syncthreads();
+
+    const float px = k.geo.wall[3 * p], py = k.geo.wall[3 * p + 1], pz = k.geo.wall[3 * p + 2];
+    const float* lin = k.geo.grid_lin + 4 * (size_t)p;
+    const float mc2 = k.opt.cutoff * k.opt.cutoff;
+    const float r0 = k.geo.r[0];
+    const float dr = nr > 1 ? (k.geo.r[nr - 1] - r0) / (float)(nr - 1) : 0.f;
+    const float inv_dr = dr > 0.f ? 1.0f / dr : 0.f;
+    int nrec = 0, qhead = 0, qcount = 0;
+#ifdef NLOSGR_SWEEP_DEBUG
+    long long dbg_got = 0, dbg_exp = 0, dbg_win = 0, dbg_pass = 0, dbg_batch = 0;
+#endif
+
+    for (int base = g_lo + wave * 64; base < g_hi; base += kBlock) {
+        Pair P;
+        float lw = 0.f;
+        bool more = false;
+        int ci = 0, cj = 0;
+        P.i0 = P.i1 = P.j0 = P.j1 = 0;
+        {
+            const int gi = base + lane;
+            const int gl = min(gi, k.g.ng - 1);
+            const GaussRec nrec_ = k.recs[gl];
+            if (gi < g_hi) {
+                float mu[3];
+                load_rec(nrec_, P, mu);
+                pair_setup<PRESET, false>(k, k.g.features + (size_t)gl * k.g.k_feat, mu, px, py, pz, lin, mc2, P);
+                more = (P.w > 0.f) && P.i0 <= P.i1 && P.j0 <= P.j1;
+                lw = more ? flog2(P.w) : 0.f;
+            }
+            ci = P.i0; cj = P.j0;
+        }
+        while (true) {
+            if (qcount < 64 && __builtin_amdgcn_ballot_w64(more)) {
+                wave_sync();
+                enumerate_box<false>(P.M, P.i1, P.j0, P.j1, more, ci, cj, tth, tph, nt - 1, rayq, qhead, qcount);
+                wave_sync();
+            }
+            const bool anymore = __builtin_amdgcn_ballot_w64(more) != 0;
+            if (qcount == 0) {
+                if (!anymore) break;
+                continue;
+            }
+            if (qcount < 64 && anymore) continue;
+            // queue entries -> segment records (lane = entry; pair data from lane `slot`)
+            const int ntake = min(64, qcount);
+            const bool take = lane < ntake;
+            const unsigned e = take ? rayq[(qhead + lane) & (kRQ - 1)] : 0u;
+            const int slot = e & 0xFF, i = (e >> 8) & 0xFFF, j = e >> 20;
+            float A[9], u0[3];
+#pragma unroll
+            for (int c = 0; c < 9; ++c) A[c] = __shfl(P.A[c], slot);
+#pragma unroll
+            for (int c = 0; c < 3; ++c) u0[c] = __shfl(P.u0[c], slot);
+            const float lws = __shfl(lw, slot);
+            bool ok = false;
+            Ray R;
+            const float2 th = tth[i], ph = tph[j];
+            if (take) ok = ray_setup<false>(A, u0, th.x * ph.x, th.x * ph.y, th.y, mc2, r0, inv_dr, nr, R);
+            qhead = (qhead + ntake) & (kRQ - 1);
+            qcount -= ntake;
+            const unsigned long long m = __builtin_amdgcn_ballot_w64(ok);
+#ifdef NLOSGR_SWEEP_DEBUG
+            if (ok) dbg_exp += R.kh - R.kl + 1;
+#endif
+            if (ok) {
+                const float ga = -kHalfLog2e * R.a * dr * dr;
+                const float al = fmaf(-kHalfLog2e, R.m2min, lws) + flog2(th.x);
+                rec[nrec + lanes_below(m)] = make_float4(ga, al, R.ks, rec_pack(R.kl, R.kh));
+            }
+            nrec += __popcll(m);
+            if (nrec > kSCap - 64) {
+                wave_sync();
+                sweep_batch(rec, idx, hidx, cnt, bcur, bend, hist, nrec, nb NLOSGR_DBG_PASS);
+#ifdef NLOSGR_SWEEP_DEBUG
+                dbg_batch += 1;
+#endif
+                nrec = 0;
+                wave_sync();
+            }
+        }
+    }
+    if (nrec > 0) {
+        wave_sync();
+        sweep_batch(rec, idx, hidx, cnt, bcur, bend, hist, nrec, nb NLOSGR_DBG_PASS);
+    }
+#ifdef NLOSGR_SWEEP_DEBUG
+    {
+        long long a = dbg_got, b = dbg_exp;
+        for (int o = 32; o > 0; o >>= 1) { a += __shfl_xor(a, o); b += __shfl_xor(b, o); }
+        if (lane == 0 && a != b && blockIdx.x < 64) printf("sweep dbg p %d split %d wave %d got %lld expect %lld\n", p, gsplit, wave, a, b);
+        if (lane == 0 && (blockIdx.x % 97) == 5)
+            printf("sweep eff p %d split %d wave %d slots %lld windows %lld eff %.3f passes %lld batches %lld\n", p, gsplit, wave,
+                   a, dbg_win, (double)a / (1024.0 * (double)(dbg_win > 0 ? dbg_win : 1)), dbg_pass, dbg_batch);
+    }
+#endif
+    __syncthreads();
+    if (k.hist_out) {
+        const float hs = k.geo.hscale[p];
+        for (int t = threadIdx.x; t < nr; t += blockDim.x) {
+            float s = 0.f;
+            for (int w = 0; w < kWaves; ++w) s += smem[w * L.wave_stride + L.hist + t];
+            if (nsp > 1)
+                k.hpart[((size_t)gsplit * k.geo.nwall + p) * nr + t] = s;
+            else
+                k.hist_out[(size_t)p * nr + t] = s * k.geo.att[t] * hs;
+        }
+    }
+}
+
 // Dense no-occlusion forward (cutoff <= 0: every Gaussian at every sample, the reference's own
 // support): every ray covers every bin, so the lane-serial drain above degenerates (all segments
 // claim the same bins; read-add-write chains bound by LDS latency).  Here lane = bin instead: a
@@ -1776,9 +2227,7 @@ int bwd_nsplit(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlos
 // sh_kernel) is bounded: NLOSGR_DRHO_MB (default 1024) MiB, i.e. C3 6.5 GB -> 1 GiB, a C5 rank 16.4 GB
 // -> 1 GiB.  Split counts are sized for one batch; batches after the first add into the partial slabs.
 int drho_batch(const nlosgr_gaussians* g, const nlosgr_geometry* geo) {
-    const char* e = getenv("NLOSGR_DRHO_MB");   // read per call (the workspace query and the launch agree)
-    const double mb = e ? atof(e) : 1024.0;
-    const long long budget = (long long)((mb > 0.0 ? mb : 1024.0) * 1048576.0);
+    const long long budget = (long long)(batch_budgets().drho_mb * 1048576.0);
     const long long per = (long long)(g->ng > 0 ? g->ng : 1) * (long long)sizeof(float);
     long long b = budget / per;
     if (b < 1) b = 1;
@@ -1808,6 +2257,13 @@ void launch_fwd(const KArgs& ka, size_t shm, hipStream_t s) {
     const char* ftail = getenv("NLOSGR_FTAIL");
     const bool tail = kCanTail && ka.opt.cutoff >= kTailCutoff && !ka.counts && !(ftail && ftail[0] == '0') &&
                       (MODE != NLOSGR_MODE_NETF || ka.opt.c_deltaT <= kSmallX);
+    // NLOSGR_FSWEEP=1: the window sweep instead of the lane-serial TAIL drain (experimental; A/B)
+    const char* fsw = getenv("NLOSGR_FSWEEP");
+    const size_t shs = (size_t)SweepLayout(ka.geo.nr, ka.geo.nt, ka.geo.np).total * sizeof(float);
+    if (tail && MODE == NLOSGR_MODE_NOOCL && !CACHE && (fsw && fsw[0] == '1') && shs <= 160 * 1024) {
+        hipLaunchKernelGGL((fwd_sweep_kernel<PRESET>), grid, dim3(kBlock), shs, s, ka);
+        return;
+    }
     if (tail) hipLaunchKernelGGL((fwd_kernel<PRESET, MODE, DENSE, RAYS, CACHE, kCanTail>), grid, dim3(kBlock), shm, s, ka);
     else hipLaunchKernelGGL((fwd_kernel<PRESET, MODE, DENSE, RAYS, CACHE>), grid, dim3(kBlock), shm, s, ka);
 }
@@ -1977,6 +2433,12 @@ int run_fwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_
 extern "C" {
 
 int nlosgr_abi_version(void) { return NLOSGR_ABI_VERSION; }
+
+void nlosgr_set_batch_budgets(double drho_mb, double tile_hpart_mb) {
+    BatchBudgets& b = batch_budgets();
+    if (drho_mb > 0.0) b.drho_mb = drho_mb;
+    if (tile_hpart_mb > 0.0) b.tile_hpart_mb = tile_hpart_mb;
+}
 
 const char* nlosgr_last_error(void) { return g_err; }
 

@@ -246,7 +246,14 @@ class TrainStep:
         """Wall-point ranges [p0, p1) of the occlusion mode's fused batches (row cache <= OCCL_BATCH_BYTES)."""
         P = self.geo.nwall
         per = max(1, tile_rows_bytes(self.geo) // max(1, P))
-        nb = max(1, OCCL_BATCH_BYTES // per)
+        budget = OCCL_BATCH_BYTES
+        if self.geo.wall.is_cuda:
+            # at most half the free device memory (the batch's row cache is allocated per batch); when
+            # not even one wall point's rows fit, the backward recomputes the forward sweep instead
+            free, _ = torch.cuda.mem_get_info(self.geo.wall.device)
+            budget = min(budget, free // 2)
+        self._occl_cache = budget >= per
+        nb = max(1, budget // per)
         return [(p0, min(P, p0 + nb)) for p0 in range(0, P, nb)]
 
     def phase_ms(self):
@@ -277,7 +284,11 @@ class TrainStep:
                 evs = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
                 self._batch_events.append(tuple(evs))
                 evs[0].record(stream)
-            hist, _, ws = render_forward(*params, geo, cfg, True, False, ray_cache=True)
+            cached = self._occl_cache
+            if cached:
+                hist, _, ws = render_forward(*params, geo, cfg, True, False, ray_cache=True)
+            else:
+                (hist, _), ws = render_forward(*params, geo, cfg, True, False), None
             if evs:
                 evs[1].record(stream)
             n_b = geo.nwall * geo.nr
@@ -285,7 +296,7 @@ class TrainStep:
             sums += loss4[2:4]
             if evs:
                 evs[2].record(stream)
-            d = render_backward(*params, geo, cfg, grad_hist=grad, workspace=ws, ray_cache=True)
+            d = render_backward(*params, geo, cfg, grad_hist=grad, workspace=ws, ray_cache=cached)
             if evs:
                 evs[3].record(stream)
             del ws, hist, grad

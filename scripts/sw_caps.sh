@@ -1,0 +1,5 @@
+set -o pipefail
+mkdir -p gpurun_out/sw5
+for L in "" ab/lib_cap256.so ab/lib_cap448.so ab/lib_cap1100.so; do
+  echo "lib=$L"; NLOSGR_LIB=$L timeout -k 10 200 python scripts/ab_env.py --reps 2 --cutoff 5.7 - NLOSGR_FSWEEP=0 2>&1 | tail -1 || exit 1
+done

@@ -317,14 +317,14 @@ def test_tile_forward_wall_batches_bitwise(monkeypatch, mode, selection):
     cfg = RenderConfig(preset="cuda", mode=mode, sh_degree=3, cutoff=5.7, c_deltaT=C * DELTAT,
                        ray_scale=1.0 if mode == "occl" else C * DELTAT, selection=selection)
     args = (m._mu, m._scaling, m._rotation, m._opacity, features_flat(m).detach())
+    from nlosgr import _lib
     out = []
-    for hp in (None, "0.0001"):
-        if hp:
-            monkeypatch.setenv("NLOSGR_TILE_HPART_MB", hp)
-        h, r, ws = render_forward(*args, geo, cfg, want_rays=True, ray_cache=mode == "occl") \
-            if mode == "occl" else (*render_forward(*args, geo, cfg, want_rays=True), None)
-        gh = torch.ones_like(h)
-        d = render_backward(*args, geo, cfg, grad_hist=gh, workspace=ws, ray_cache=ws is not None)
+    for hp in (None, 0.0001):
+        with _lib.batch_budgets(tile_hpart_mb=hp):
+            h, r, ws = render_forward(*args, geo, cfg, want_rays=True, ray_cache=mode == "occl") \
+                if mode == "occl" else (*render_forward(*args, geo, cfg, want_rays=True), None)
+            gh = torch.ones_like(h)
+            d = render_backward(*args, geo, cfg, grad_hist=gh, workspace=ws, ray_cache=ws is not None)
         out.append((h, r, d))
     (h0, r0, d0), (h1, r1, d1) = out
     assert torch.equal(h0, h1) and torch.equal(r0, r1)

@@ -340,7 +340,8 @@ def test_backward_wall_batches_equal_single_batch(monkeypatch):
     grad = torch.randn_like(hist)
     ref = render_backward(*args, geo, cfg, grad_hist=grad)
     # 1500 Gaussians x 4 B x 11 wall points per batch: 30 wall points -> 3 batches
-    monkeypatch.setenv("NLOSGR_DRHO_MB", str(1500 * 4 * 11 / 1048576.0))
-    got = render_backward(*args, geo, cfg, grad_hist=grad)
+    from nlosgr import _lib
+    with _lib.batch_budgets(drho_mb=1500 * 4 * 11 / 1048576.0):
+        got = render_backward(*args, geo, cfg, grad_hist=grad)
     for a, b in zip(got, ref):
         assert _rel(a, b) <= 1e-5
