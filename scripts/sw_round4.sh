@@ -1,5 +1,6 @@
 set -o pipefail
 mkdir -p gpurun_out/sw6
+timeout -k 10 600 python -u -m pytest tests/test_gpu_fullsize.py -x -q --timeout 300 --timeout-method thread -k "c3_full_size_train or c3_occl" > gpurun_out/sw6/full.log 2>&1; tail -5 gpurun_out/sw6/full.log
 timeout -k 10 200 python scripts/sweep_diag2.py > gpurun_out/sw6/d2.log 2>&1; tail -4 gpurun_out/sw6/d2.log
 timeout -k 10 300 python -u -m pytest tests/test_gpu_sweep.py -x -q --timeout 120 --timeout-method thread > gpurun_out/sw6/tests.log 2>&1; tail -3 gpurun_out/sw6/tests.log
 NLOSGR_FSWEEP=1 NLOSGR_LIB=ab/lib_dbg.so timeout -k 10 200 python scripts/ab_env.py --reps 0 --cutoff 5.7 - > gpurun_out/sw6/eff.log 2>&1 || exit 1

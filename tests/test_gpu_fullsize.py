@@ -174,10 +174,17 @@ def test_c3_full_size_train_step_parity():
     for t in d:
         assert torch.isfinite(t).all()
     _culled_vs_dense(m, scene, "cuda", idx, hist, d, gseed)
+    # a 100-Gaussian subset on the full geometry vs the oracle: histogram of the 2 wall points and the
+    # gradients of all six raw tensors seeded there (the culled 5.7 sigma kernels, as in the step)
     sub = _subset(m, torch.arange(0, 100_000, 1000, device=dev))
-    hs, _ = render_forward(*_params(sub), geo, make_config(sub, scene, "cuda", "noocl", cutoff=PARITY_CUTOFF))
-    ref, _ = _oracle(sub, scene, idx.cpu(), "cuda", "noocl", PARITY_CUTOFF)
+    scfg = make_config(sub, scene, "cuda", "noocl", cutoff=PARITY_CUTOFF)
+    hs, _ = render_forward(*_params(sub), geo, scfg)
+    ds = render_backward(*_params(sub), geo, scfg, grad_hist=gfull)
+    ref, rgrads = _oracle(sub, scene, idx.cpu(), "cuda", "noocl", PARITY_CUTOFF, gout=gseed.cpu())
     _close(hs[idx], ref, 2e-5, msg="C3 subset hist")
+    for name, a, b in zip(("mu", "scaling", "rotation", "opacity", "dc", "rest"), _hip_grads_as_ref(ds), rgrads):
+        assert float(b.abs().max()) > 0 or name == "rest", name
+        _close(a, b, 2e-4, atol=1e-9, msg=f"C3 subset grad {name}")
 
 
 def test_c4_full_size_binint_vs_numerical():
@@ -303,6 +310,8 @@ def test_c3_occl_full_size():
                                               sub._features_dc, sub._features_rest)), 3, requires_grad=False)
     bb = bboxes(sub._mu, sub._scaling, sub._rotation, 1.0, 3.0, preset="cuda").reshape(-1, 6).cpu()
     feats = P.features[:, :, 0]
+    gs = torch.randn(len(idx), 1024, generator=torch.Generator().manual_seed(11))
+    refs = []
     for w, p in enumerate(idx.tolist()):
         pw = scene.walls("cpu")[p]
         tab = R.sample_tables(pw, scene.box("cpu"), scene.ns, scene.start, scene.end, scene.c, scene.deltaT)
@@ -317,10 +326,43 @@ def test_c3_occl_full_size():
         ref = res.sum(1) * tab["dtheta"] * tab["dphi"] * scene.volume_position[1] ** 2
         assert float(ref.abs().max()) > 0
         _close(hs[w], ref, 2e-4, msg=f"C3 occl aabb subset wall point {p}")
+        refs.append(ref)
     del d
+    # ... and the subset's gradients seeded on those wall points vs torch autograd of the restatement
+    # (path C's own backward returns zeros: cuda_autograd.py:147-156)
+    P2 = R.Params(*(t.detach().cpu() for t in (sub._mu, sub._scaling, sub._rotation, sub._opacity,
+                                               sub._features_dc, sub._features_rest)), 3, requires_grad=True)
+    feats2 = P2.features[:, :, 0]
+    loss = 0.0
+    for w, p in enumerate(idx.tolist()):
+        pw = scene.walls("cpu")[p]
+        tab = R.sample_tables(pw, scene.box("cpu"), scene.ns, scene.start, scene.end, scene.c, scene.deltaT)
+        tg, pg = torch.meshgrid(tab["theta"], tab["phi"], indexing="ij")
+        tf, pf = tg.reshape(-1), pg.reshape(-1)
+        dr = torch.stack([torch.sin(tf) * torch.cos(pf), torch.sin(tf) * torch.sin(pf), torch.cos(tf)], 1)
+        o = pw.unsqueeze(0).expand(dr.shape[0], 3).contiguous()
+        t = torch.linspace(tab["I1"] * scene.c * scene.deltaT, tab["I2"] * scene.c * scene.deltaT, tab["nr"])
+        rho, _, _ = R.render_rays_cuda(o, dr, t, P2, feats2, pw, 3, scene.c, scene.deltaT, 1.0, True,
+                                       R.aabb_filter(o, dr, bb))
+        res = rho.T / (t.view(-1, 1) ** 2 + 1e-8) * torch.sin(tf).view(1, -1)
+        loss = loss + ((res.sum(1) * tab["dtheta"] * tab["dphi"] * scene.volume_position[1] ** 2) * gs[w]).sum()
+    loss.backward()
+    dsub = render_backward(*_params(sub), gsel, make_config(sub, scene, "cuda", "occl", cutoff=PARITY_CUTOFF,
+                                                            selection="aabb"), grad_hist=gs.to(dev))
+    for name, a, b in zip(("mu", "scaling", "rotation", "opacity", "dc", "rest"), _hip_grads_as_ref(dsub),
+                          P2.leaves()):
+        _close(a, b.grad, 3e-4, atol=1e-9, msg=f"C3 occl aabb subset grad {name}")
     # 5.7 sigma support: whole forward volume, 2 wall points vs the dense evaluation
     cfg_s = make_config(m, scene, "cuda", "occl", cutoff=PARITY_CUTOFF)
     hist, _ = render_forward(*_params(m), geo, cfg_s)
     _finite_volume(hist)
-    ref, _ = render_forward(*_params(m), gsel, make_config(m, scene, "cuda", "occl", cutoff=0.0))
+    dcfg = make_config(m, scene, "cuda", "occl", cutoff=0.0)
+    ref, _ = render_forward(*_params(m), gsel, dcfg)
     _close(hist[idx], ref, 2e-5, msg="C3 occl 5.7 sigma vs dense")
+    # the 5.7 sigma occlusion backward seeded on those 2 wall points vs the dense backward there
+    # (every Gaussian of the 100k in the shared-transmittance scan)
+    d57 = render_backward(*_params(m), gsel, cfg_s, grad_hist=gs.to(dev) * 1e-3)
+    dd = render_backward(*_params(m), gsel, dcfg, grad_hist=gs.to(dev) * 1e-3)
+    for name, a, b in zip(("mu", "scaling", "rotation", "opacity", "features"), d57, dd):
+        assert torch.isfinite(a).all() and float(b.abs().max()) > 0
+        _close(a, b, 3e-4, atol=1e-12, msg=f"C3 occl 5.7 sigma vs dense grad {name}")
