@@ -334,7 +334,7 @@ __device__ __forceinline__ bool drain_setup(const float* A, const float* u0, flo
     } else if (MODE == NLOSGR_MODE_BININT) {
         // bin average of exp(-a (r - t*)^2 / 2) over [r_k -+ dr/2] = sqrt(pi)/(2 beta) (erf(x1) - erf(x0))
         d.beta = dr * sqrtf(0.5f * R.a);
-        d.al = fmaf(-kHalfLog2e, R.m2min, lw) + log2f(0.88622692545275801f / d.beta);
+        d.al = fmaf(-kHalfLog2e, R.m2min, lw);   // the erf form's sqrt(pi) / (2 beta) is applied per value
         if (!RAYS) d.al += flog2(th.x);
         d.st = th.x;
         d.xlo = d.beta * (d.t - 0.5f);
@@ -442,6 +442,7 @@ __device__ __forceinline__ void compiler_fence() { __asm__ __volatile__("" ::: "
 // Gaussian's peak (<= 3.7e-6 at m_c >= kTailCutoff), so the result lies between the culled and the
 // dense sum.  Bins past nr land in the zeroed pad row.
 constexpr float kTailCutoff = 5.0f;
+constexpr float kBetaSeries = 0.5f;   // bin-integrated TAIL drain: series bin average up to this beta
 
 template <int PRESET, int MODE, bool DENSE, bool RAYS, bool CACHE, bool TAIL = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) void fwd_kernel(KArgs k) {
@@ -481,7 +482,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
     const float rscale = k.opt.ray_scale;
     const int flags = k.opt.flags;
     // the float2 drain (two bins per LDS read-add-write; claim keys on bin pairs)
-    constexpr bool QUADF = (MODE == NLOSGR_MODE_NOOCL || (MODE == NLOSGR_MODE_NETF && TAIL)) && !RAYS && !DENSE;
+    constexpr bool QUADF = (MODE == NLOSGR_MODE_NOOCL || ((MODE == NLOSGR_MODE_NETF || MODE == NLOSGR_MODE_BININT) && TAIL)) &&
+                           !RAYS && !DENSE;
     const int pad = nr + kSteps + lane;       // this lane's private pad bins (non-winners)
     const int padq = al4(nr + kSteps);        // quad drain: one pad quad row shared by non-winners (they add 0)
     unsigned npair = 0, nseg = 0;
@@ -614,6 +616,51 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
                         hb2[kv] = x;
                         compiler_fence();
                     }
+                } else if (TAIL && win && MODE == NLOSGR_MODE_BININT) {
+                    // bin-integrated (C4), TAIL: the average of exp(-beta^2 t^2) over the bin [t - 1/2, t + 1/2]
+                    // (t in bins from the closest approach, beta = dr sqrt(a / 2)) is g(t) (1 + sum_n g^(2n)(t) /
+                    // (2^2n (2n+1)!) / g(t)) = g(t) P(beta^2 t^2), P a cubic from the n <= 3 terms: relative error
+                    // <= 7e-8 for beta <= kBetaSeries (a Gaussian wider than 1.4 bins along the ray), so g comes
+                    // from the exp2 recurrence as in the numerical drain and each bin costs a cubic instead of
+                    // two erfc.  Narrower rays (beta > kBetaSeries) take the erf difference, when a round holds one.
+                    const float b = d.beta * d.beta;
+                    const float c3 = b * b * b * (1.0f / 5040.0f);
+                    const float c2 = b * b * fmaf(b, -1.0f / 672.0f, 1.0f / 120.0f);
+                    const float c1 = b * fmaf(b, fmaf(b, 1.0f / 448.0f, -1.0f / 40.0f), 1.0f / 6.0f);
+                    const float c0 = fmaf(b, fmaf(b, fmaf(b, -1.0f / 2688.0f, 1.0f / 160.0f), -1.0f / 12.0f), 1.0f);
+                    const float t0 = t - (float)o;    // t of slot 0
+                    float cur = fast_exp2(fmaf(d.ga, t * t, d.al));
+                    float q = fast_exp2(d.ga * fmaf(2.f, t, 1.f));
+                    const float cc = fast_exp2(2.f * d.ga);
+                    const bool series = d.beta <= kBetaSeries;
+                    const bool anyerf = __builtin_amdgcn_ballot_w64(!series) != 0;   // (EXEC = the winners)
+                    const float pref = fast_exp2(d.al) * (0.88622692545275801f * frcp(d.beta));
+                    float2* hb2 = reinterpret_cast<float2*>(hb);
+#pragma unroll
+                    for (int kv = 0; kv < kSteps / VW; ++kv) {
+                        float v[VW];
+#pragma unroll
+                        for (int jj = 0; jj < VW; ++jj) {
+                            const int jslot = VW * kv + jj;
+                            const float tj = t0 + (float)jslot;
+                            const float u = b * tj * tj;
+                            float val = cur * fmaf(u, fmaf(u, fmaf(u, c3, c2), c1), c0);
+                            if (anyerf && !series) {
+                                const float x0 = d.beta * (tj - 0.5f), x1 = d.beta * (tj + 0.5f);
+                                const float e0 = erfcf(fabsf(x0)), e1 = erfcf(fabsf(x1));
+                                const float df = x0 >= 0.f ? e0 - e1 : (x1 <= 0.f ? e1 - e0 : 2.0f - e0 - e1);
+                                val = pref * df;
+                            }
+                            const bool pre = kv == 0 && jj < o;   // slot before pos (first round of a segment)
+                            v[jj] = pre ? 0.f : val;
+                            cur = pre ? cur : cur * q;
+                            q = pre ? q : q * cc;
+                        }
+                        float2 x = hb2[kv];
+                        x.x += v[0]; x.y += v[1];
+                        hb2[kv] = x;
+                        compiler_fence();
+                    }
                 } else if (TAIL && win) {
                     // netf, TAIL: out_k = w c dT sin(theta) pdf_k T_k, T_{k+1} = T_k (exp(-sigma pdf_k c dT)
                     // + 1e-7), two bins per float2 read-add-write; slot 0 before pos (o = 1, a segment's
@@ -709,7 +756,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
                     const float df = xlo >= 0.f ? elo - e1 : (x1 <= 0.f ? e1 - elo : 2.0f - elo - e1);
                     xlo = x1;
                     elo = e1;
-                    const float pv = fast_exp2(d.al) * df;
+                    const float pv = fast_exp2(d.al) * (0.88622692545275801f * frcp(d.beta)) * df;
                     v = in ? pv : 0.f;
                     if (RAYS) {
                         if (in) atomicAdd(rout + d.rbase + d.pos + m, rscale * pv);
@@ -2251,7 +2298,8 @@ int bwd_nsplit_ws(const nlosgr_gaussians* g, const nlosgr_geometry* geo0, const 
 template <int PRESET, int MODE, bool DENSE, bool RAYS, bool CACHE>
 void launch_fwd(const KArgs& ka, size_t shm, hipStream_t s) {
     const dim3 grid(ka.geo.nwall, ka.hpart ? ka.nfsplit : 1);
-    constexpr bool kCanTail = (MODE == NLOSGR_MODE_NOOCL || MODE == NLOSGR_MODE_NETF) && !DENSE && !RAYS;
+    constexpr bool kCanTail = (MODE == NLOSGR_MODE_NOOCL || MODE == NLOSGR_MODE_NETF || MODE == NLOSGR_MODE_BININT) &&
+                              !DENSE && !RAYS;
     // NLOSGR_FTAIL=0: masked forward drain at every cutoff (A/B and parity cross-check); netf takes the
     // TAIL drain where its backward does (c dT <= 1/64), so both see the same support
     const char* ftail = getenv("NLOSGR_FTAIL");

@@ -110,9 +110,10 @@ def test_section_renderer_dropin():
 
 
 @pytest.mark.parametrize("preset", ["cuda", "torch"])
-@pytest.mark.parametrize("cutoff", [0.0, 3.0])
+@pytest.mark.parametrize("cutoff", [0.0, 3.0, 5.7])
 def test_binint_volume_vs_oracle(preset, cutoff):
-    """Bin-integrated forward (mode "binint") vs the float64 oracle, same support rule."""
+    """Bin-integrated forward (mode "binint") vs the float64 oracle, same support rule (at cutoff >= 5
+    the TAIL drain: the series bin average for rays wider than 1.4 bins, erf differences below)."""
     from nlosgr import GaussianParams, features_flat
     from nlosgr.geometry import build_geometry, relay_wall_grid, volume_box_point
     from nlosgr.render import RenderConfig, render_forward
@@ -134,6 +135,32 @@ def test_binint_volume_vs_oracle(preset, cutoff):
     ref = R.render_volume_binint(P, walls.cpu(), box.cpu(), 0.5, ns, start, end, c, deltaT, preset,
                                  mc=cutoff if cutoff > 0 else None)
     _close(hist.cpu(), ref, 5e-5, 1e-9, f"binint {preset} mc={cutoff}")
+
+
+@pytest.mark.parametrize("shift", [-2.5, 0.0, 1.2])
+def test_binint_tail_series_and_erf_rays(shift):
+    """The binint TAIL drain (cutoff 5.7) on Gaussians from sub-bin (every ray on the erf path) through
+    mixed rounds to many bins wide (series path) vs the float64 oracle (T = 96)."""
+    from nlosgr import GaussianParams, features_flat
+    from nlosgr.geometry import build_geometry, relay_wall_grid, volume_box_point
+    from nlosgr.render import RenderConfig, render_forward
+    from oracle import torch_ref as R
+    dev = torch.device("cuda:0")
+    ng, deg, ns, T = 40, 3, 6, 96
+    c, deltaT = 1.0, 1.28 / T
+    start, end = T // 8, T // 8 + T
+    m = GaussianParams.synthetic(ng, deg, preset="cuda", device=dev, seed=8)
+    with torch.no_grad():
+        m._scaling.add_(shift + 0.6 * torch.randn(m._scaling.shape, generator=torch.Generator().manual_seed(1)).to(dev))
+    walls = relay_wall_grid(2, 2, device=dev)
+    box = volume_box_point((0.0, 0.5, 0.0), 0.5, dev)
+    geo = build_geometry(walls, box, ns, start, end, c, deltaT, 0.5, "cuda", "binint")
+    cfg = RenderConfig(preset="cuda", mode="binint", sh_degree=deg, cutoff=5.7, c_deltaT=c * deltaT)
+    hist, _ = render_forward(m._mu, m._scaling, m._rotation, m._opacity, features_flat(m), geo, cfg)
+    P = _oracle_params(m, deg)
+    ref = R.render_volume_binint(P, walls.cpu(), box.cpu(), 0.5, ns, start, end, c, deltaT, "cuda", mc=5.7)
+    assert float(ref.abs().max()) > 0
+    _close(hist.cpu(), ref, 5e-5, 1e-9, f"binint TAIL shift {shift}")
 
 
 def test_binint_backward_unsupported():
