@@ -62,15 +62,35 @@ class CUDARenderFunction(torch.autograd.Function):
                 None, None, None, None, None, None, None) + (None,) * ctx.nextra
 
 
+def reference_sh_rows(features: torch.Tensor, degree: int) -> torch.Tensor:
+    """The coefficient rows the reference's path C kernel actually reads: it is handed the dc features
+    only, [N, C] (cuda_autograd.py:276-280, sh_dim = C), and eval_sh reads (degree + 1)^2 consecutive
+    floats from g * sh_dim (volume_renderer.cu:110,170, spherical_harmonics.cuh:64-80), i.e. for
+    degree > 0 the dc values of the following Gaussians.  Row g of the result is flat[g*C : g*C + K]
+    of the flattened features, K = (degree + 1)^2; reads past the last Gaussian (out of bounds in the
+    reference) are zero here.  Differentiable (a gather): gradients flow back to the dc tensor."""
+    n, c = features.shape
+    k = (int(degree) + 1) ** 2
+    flat = features.reshape(-1)
+    idx = torch.arange(n, device=features.device).unsqueeze(1) * c + torch.arange(k, device=features.device)
+    valid = idx < flat.numel()
+    return flat[idx.clamp(max=max(flat.numel() - 1, 0))] * valid.to(features.dtype)
+
+
 class CUDARenderModule(nn.Module):
     """Spherical ray grid from one relay-wall point, geometric attenuation and angular integration
-    around CUDARenderFunction (cuda_autograd.py:194-316)."""
+    around CUDARenderFunction (cuda_autograd.py:194-316).
 
-    def __init__(self, sigma_threshold: float = 3.0):
+    reference_sh_reads=True reproduces the reference's SH evaluation at active_sh_degree > 0 as it
+    actually runs (neighbouring Gaussians' dc values as higher-order coefficients, reference_sh_rows);
+    the default evaluates the dc features at degree 0 (the intent of passing dc only)."""
+
+    def __init__(self, sigma_threshold: float = 3.0, reference_sh_reads: bool = False):
         super().__init__()
         if not CUDA_AVAILABLE:
             raise RuntimeError("CUDA renderer not available")
         self.sigma_threshold = sigma_threshold
+        self.reference_sh_reads = reference_sh_reads
 
     def forward(self, gaussian_model, camera_pos: torch.Tensor, theta_range: Tuple[float, float],
                 phi_range: Tuple[float, float], r_range: Tuple[float, float], num_theta: int, num_phi: int,
@@ -86,10 +106,13 @@ class CUDARenderModule(nn.Module):
         t_samples = torch.linspace(r_range[0], r_range[1], num_r, device=device)
         # the reference passes the dc features only (cuda_autograd.py:276-280)
         features = gaussian_model.get_features_dc.squeeze(1)
+        deg = int(gaussian_model.active_sh_degree)
+        if self.reference_sh_reads and deg > 0:
+            features = reference_sh_rows(features, min(deg, 3))
         rho, _, _ = CUDARenderFunction.apply(ray_origins, ray_dirs, t_samples, gaussian_model.get_mu,
                                              gaussian_model._scaling, gaussian_model._rotation,
                                              gaussian_model._opacity, features, camera_pos,
-                                             gaussian_model.active_sh_degree, c, deltaT, scaling_modifier,
+                                             deg, c, deltaT, scaling_modifier,
                                              use_occlusion, rendering_type, self.sigma_threshold)
         result = rho.T.reshape(num_r, num_theta, num_phi)
         distance = t_samples.view(-1, 1, 1)
@@ -100,8 +123,9 @@ class CUDARenderModule(nn.Module):
         return result, pred_histogram
 
 
-def create_cuda_render_module(sigma_threshold: float = 3.0) -> Optional[CUDARenderModule]:
+def create_cuda_render_module(sigma_threshold: float = 3.0,
+                              reference_sh_reads: bool = False) -> Optional[CUDARenderModule]:
     """CUDARenderModule if the HIP library and a GPU are available, else None (:319-331)."""
     if not CUDA_AVAILABLE:
         return None
-    return CUDARenderModule(sigma_threshold=sigma_threshold)
+    return CUDARenderModule(sigma_threshold=sigma_threshold, reference_sh_reads=reference_sh_reads)

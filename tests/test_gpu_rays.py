@@ -155,6 +155,48 @@ def test_render_module_dropin():
         _close(leaf.grad, rleaf.grad, 2e-4, atol=1e-6, msg=f"grad {name}")
 
 
+@pytest.mark.parametrize("deg", [1, 3])
+def test_render_module_reference_sh_reads(deg):
+    """CUDARenderModule(reference_sh_reads=True) at active_sh_degree > 0 reproduces what the reference
+    kernel computes with dc-only features (spherical_harmonics.cuh:64-80 with sh_dim = 1: Gaussian g
+    reads the dc values of g .. g + K - 1; zero past the end): forward and the gradients (to dc
+    through the gather) vs the oracle fed the same rows; the default module evaluates degree 0."""
+    from nlosgr.cuda_autograd import CUDARenderModule, reference_sh_rows
+    from oracle import torch_ref as R
+    dev = torch.device("cuda:0")
+    m, _, _ = _scene(40, 1, 33, scale_shift=1.2, deg=3)
+    m.active_sh_degree = deg
+    cam = torch.tensor([0.1, 0.0, -0.1], device=dev)
+    tr_, pr_ = (0.4, 1.6), (0.9, 2.3)
+    nt, npp, nr, c, dT = 8, 6, 40, 1.0, 0.03
+    mod = CUDARenderModule(reference_sh_reads=True)
+    result, hist = mod(m, cam, tr_, pr_, (0.2, 1.4), nt, npp, nr, c, dT, 1.0, False, "netf")
+    P, _ = _oracle(m, deg)
+    rows = reference_sh_rows(P._features_dc[:, :, 0], deg)
+    K = (deg + 1) ** 2
+    assert rows.shape == (40, K) and float(rows[-1, 1:].detach().abs().max()) == 0.0   # past the end: zero
+    assert torch.equal(rows[0, 1:].detach(), P._features_dc[1:K, 0, 0].detach())     # neighbours' dc
+    theta = torch.linspace(*tr_, nt)
+    phi = torch.linspace(*pr_, npp)
+    tg, pg = torch.meshgrid(theta, phi, indexing="ij")
+    tf, pf = tg.reshape(-1), pg.reshape(-1)
+    d = torch.stack([torch.sin(tf) * torch.cos(pf), torch.sin(tf) * torch.sin(pf), torch.cos(tf)], 1)
+    o = cam.cpu().unsqueeze(0).expand(tf.shape[0], 3).contiguous()
+    t = torch.linspace(0.2, 1.4, nr)
+    filt = R.aabb_filter(o, d, R.bboxes_cuda(P))
+    rho, _, _ = R.render_rays_cuda(o, d, t, P, rows, cam.cpu(), deg, c, dT, 1.0, False, filt)
+    ref = rho.T.reshape(nr, nt, npp) / (t.view(-1, 1, 1) ** 2 + 1e-8) * torch.sin(tg.unsqueeze(0))
+    ref_h = ref.sum(dim=(1, 2)) * ((tr_[1] - tr_[0]) / nt) * ((pr_[1] - pr_[0]) / npp)
+    _close(hist, ref_h, 2e-5, msg=f"hist deg {deg}")
+    hist.sum().backward()
+    ref_h.sum().backward()
+    _close(m._features_dc.grad, P._features_dc.grad, 2e-4, atol=1e-6, msg="grad features_dc")
+    _close(m._mu.grad, P._mu.grad, 2e-4, atol=1e-6, msg="grad mu")
+    # the default module: degree-0 evaluation, which differs once the neighbours' terms matter
+    _, h0 = CUDARenderModule()(m, cam, tr_, pr_, (0.2, 1.4), nt, npp, nr, c, dT, 1.0, False, "netf")
+    assert float((h0.detach() - hist.detach()).abs().max()) > 1e-6 * float(hist.abs().max())
+
+
 @pytest.mark.parametrize("occl", [False, True])
 def test_nlos_gaussian_renderer_dropin(occl):
     """NLOSGaussianRenderer (submodules/cuda_renderer/__init__.py:24-180): render() against the
