@@ -110,6 +110,29 @@ def allreduce_step(grads, loss4, n_total, group=None, async_op=False):
     return finish()
 
 
+def slab_order(mu, wall, slabs=16, cells=8):
+    """Permutation of the Gaussians for the backward: sorted by cell of a slabs x cells x cells grid over
+    their bounding box, slab (the coordinate axis along which the Gaussians lie in front of the relay
+    wall: the largest component of centroid(mu) - centroid(wall)) major, then the other two axes in
+    order.  The backward's workgroups own 64 consecutive Gaussians; spatially compact blocks have alike
+    candidate boxes and ray counts at every wall point (the block's enumeration and drain end together
+    instead of waiting for its largest pair) and share Gaussian-record cache lines: C3 backward 1136 ->
+    933 ms (scripts/order_ab.py; a Morton order gives 939, depth alone 976).  Any order gives the same
+    gradients up to fp32 summation order.  Rank-consistent: the ranks of a wall shard hold the same
+    Gaussians and their bands' centroids pick the same axis, so their permutations agree (the bucketed
+    all-reduce sums rows in this order)."""
+    with torch.no_grad():
+        d = mu.mean(0) - wall.reshape(-1, 3).mean(0)
+        k = int(torch.argmax(d.abs()))
+        axes = [k] + [i for i in range(3) if i != k]
+        q = mu[:, axes]
+        lo, hi = q.min(0).values, q.max(0).values
+        n = torch.tensor([slabs, cells, cells], device=mu.device, dtype=q.dtype)
+        cell = ((q - lo) / (hi - lo).clamp_min(1e-12) * n).floor().clamp(max=n - 1).long()
+        key = (cell[:, 0] * cells + cell[:, 1]) * cells + cell[:, 2]
+        return torch.argsort(key, stable=True)
+
+
 def bucket_bounds(ng, nbuckets):
     """Gaussian ranges [g0, g1) of the bucketed gradient exchange; g0 is a multiple of 256 (the
     backward's Gaussian-block granularity, nlosgr_options.g_begin)."""
@@ -192,8 +215,10 @@ class TrainStep:
     """
 
     def __init__(self, model, geo, cfg, target, gt_times=1.0, opt=None, spatial_lr_scale=1.0, nwall_total=None,
-                 group=None, sh_schedule=False, events=None, buckets=4, keep_grads=False):
+                 group=None, sh_schedule=False, events=None, buckets=4, keep_grads=False, bwd_order="slab"):
         self.model, self.geo, self.cfg = model, geo, cfg
+        # backward Gaussian order (slab_order; None = as stored); NLOSGR_BWD_ORDER=0 disables (A/B)
+        self.bwd_order = None if os.environ.get("NLOSGR_BWD_ORDER") == "0" else bwd_order
         self.keep_grads = keep_grads   # tests: keep the last step's (all-reduced) gradients in self.grads
         self.grads = None
         self.target = target.detach().float().contiguous()
@@ -335,6 +360,22 @@ class TrainStep:
             ev["bwd"][0].record(stream)
         bounds = bucket_bounds(ng, self.buckets) if (self.world > 1 and cfg.mode != "occl"
                                                      and cfg.selection == "support") else [(0, ng)]
+        # the backward renders the Gaussians in slab order (not with the ray cache: its records are
+        # indexed by the forward's order); its gradients are scattered back below
+        perm = None
+        if self.bwd_order == "slab" and not cache and cfg.mode != "occl" and cfg.selection == "support" and ng > 64:
+            perm = slab_order(args[0], self.geo.wall)
+            args = tuple(t[perm].contiguous() for t in args[:5]) + (args[5],)
+
+        def unperm(gs):
+            if perm is None:
+                return gs
+            out = []
+            for gr in gs:
+                o = torch.empty_like(gr)
+                o[perm] = gr
+                out.append(o)
+            return out
         if len(bounds) > 1:
             # bucketed: differentiate Gaussians [g0, g1), then all-reduce that bucket asynchronously
             # while the next bucket's backward runs (SURVEY §8e overlap)
@@ -349,12 +390,13 @@ class TrainStep:
             dist.all_reduce(sums, op=dist.ReduceOp.SUM, group=self.group)
             if ev:
                 ev["bwd"][1].record(stream)
-            grads = ex.finish()
+            grads = unperm(ex.finish())
             se, st = sums[0], sums[1]
             loss2 = torch.stack([se / float(self.n_total), torch.where(st > 0, se / st, torch.zeros_like(se))])
             del ws
         else:
-            d_mu, d_s, d_q, d_o, d_f = render_backward(*args, cfg, grad_hist=grad, workspace=ws, ray_cache=cache)
+            d_mu, d_s, d_q, d_o, d_f = unperm(render_backward(*args, cfg, grad_hist=grad, workspace=ws,
+                                                              ray_cache=cache))
             if ev:
                 ev["bwd"][1].record(stream)
             del ws

@@ -16,9 +16,11 @@ scene = Scene(H=H, W=H, T=T, ns=32)
 m = GaussianParams.synthetic(ng, 3, preset="cuda", device=dev, seed=0)
 geo = scene.geometry(dev, "cuda")
 args = (m._mu.detach(), m._scaling.detach(), m._rotation.detach(), m._opacity.detach(), features_flat(m).detach(), geo)
-base = make_config(m, scene, cutoff=3.0)
-hist, _, ws = render_forward(*args, dataclasses.replace(base, flags=ff), ray_cache=True)
+base = make_config(m, scene, cutoff=float(os.environ.get("PHASE_CUTOFF", "3.0")))
+ray_cache = os.environ.get("PHASE_CACHE", "1") == "1"
+out = render_forward(*args, dataclasses.replace(base, flags=ff), ray_cache=ray_cache)
+hist, ws = out[0], (out[2] if ray_cache else None)
 grad = torch.randn_like(hist) * 1e-3
-render_backward(*args, dataclasses.replace(base, flags=bf), grad_hist=grad, workspace=ws, ray_cache=True)
+render_backward(*args, dataclasses.replace(base, flags=bf), grad_hist=grad, workspace=ws, ray_cache=ray_cache)
 torch.cuda.synchronize()
 print("done", ff, bf)

@@ -1,0 +1,27 @@
+"""slab_order (nlosgr.train): the backward's Gaussian order is a permutation, deterministic, groups
+Gaussians by depth slab along the axis facing the relay wall, and is the same for every wall band
+of a row-interleaved shard (the bucketed all-reduce relies on it)."""
+import torch
+
+from conftest import ROOT  # noqa: F401
+
+
+def test_slab_order_permutation_and_bands():
+    from nlosgr.distributed import wall_rows
+    from nlosgr.geometry import relay_wall_grid
+    from nlosgr.model import GaussianParams
+    from nlosgr.train import slab_order
+    m = GaussianParams.synthetic(5000, 3, preset="cuda", device="cpu", seed=4)
+    mu = m._mu.detach()
+    walls = relay_wall_grid(32, 32)
+    perm = slab_order(mu, walls)
+    assert torch.equal(torch.sort(perm).values, torch.arange(5000))
+    assert torch.equal(perm, slab_order(mu, walls))
+    # depth (y: the volume sits at y = 0.5 in front of the wall) is non-decreasing in 16 slabs
+    y = mu[perm, 1]
+    slab = ((y - y.min()) / (y.max() - y.min()) * 16).floor().clamp(max=15)
+    assert bool((slab[1:] >= slab[:-1]).all())
+    for world in (2, 8):
+        for r in range(world):
+            band = walls[wall_rows(32, 32, r, world)]
+            assert torch.equal(slab_order(mu, band), perm)
