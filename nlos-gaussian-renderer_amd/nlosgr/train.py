@@ -364,7 +364,9 @@ class TrainStep:
         # indexed by the forward's order); its gradients are scattered back below
         perm = None
         if self.bwd_order == "slab" and not cache and cfg.mode != "occl" and cfg.selection == "support" and ng > 64:
-            perm = slab_order(args[0], self.geo.wall)
+            sl = os.environ.get("NLOSGR_SLAB")   # "slabs,cells" (A/B of the grid; default 16,8)
+            sc = tuple(int(v) for v in sl.split(",")) if sl else (16, 8)
+            perm = slab_order(args[0], self.geo.wall, *sc)
             args = tuple(t[perm].contiguous() for t in args[:5]) + (args[5],)
 
         def unperm(gs):
