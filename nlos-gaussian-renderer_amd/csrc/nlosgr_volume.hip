@@ -442,6 +442,13 @@ __device__ __forceinline__ void compiler_fence() { __asm__ __volatile__("" ::: "
 // Gaussian's peak (<= 3.7e-6 at m_c >= kTailCutoff), so the result lies between the culled and the
 // dense sum.  Bins past nr land in the zeroed pad row.
 constexpr float kTailCutoff = 5.0f;
+// debug build (-DNLOSGR_FCOUNT, scripts/drain_counts.py): count_support runs the TAIL forward and returns
+// (wave drain rounds, active lanes summed over rounds, claim winners summed) instead of its work counts
+#ifdef NLOSGR_FCOUNT
+#define NLOSGR_FCOUNT_ON 1
+#else
+#define NLOSGR_FCOUNT_ON 0
+#endif
 constexpr float kBetaSeries = 0.5f;   // bin-integrated TAIL drain: series bin average up to this beta
 
 template <int PRESET, int MODE, bool DENSE, bool RAYS, bool CACHE, bool TAIL = false>
@@ -522,7 +529,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
                 wc = more ? P.w * cdt : 0.f;
             }
             if (flags & 2) more = false;      // diagnostics: pair setup only
-            npair += __builtin_popcountll(__builtin_amdgcn_ballot_w64(more));
+            npair += NLOSGR_FCOUNT_ON ? 0u : (unsigned)__builtin_popcountll(__builtin_amdgcn_ballot_w64(more));
             ci = P.i0; cj = P.j0;
         }
         while (true) {
@@ -555,11 +562,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
                     const int stag = dense_wrap<MODE, DENSE>() ? (int)(((unsigned)(qhead + r) * 37u) % (unsigned)nr) : 0;
                     got = drain_setup<MODE, DENSE, RAYS>(A, u0, lws, scs, wcs, tth[i], tph[j], i, j, np_, nr, mc2,
                                                          r0, dr, inv_dr, f0log2, d, stag);
-                    if (got) nsamp += (unsigned)(d.rem + (dense_wrap<MODE, DENSE>() ? d.wrap : 0));
+                    if (got && !NLOSGR_FCOUNT_ON) nsamp += (unsigned)(d.rem + (dense_wrap<MODE, DENSE>() ? d.wrap : 0));
                     if (MODE == NLOSGR_MODE_NETF && TAIL && QUADF) d.T *= d.wc;   // the weight rides on T
                     act = got && !(flags & 4);    // diagnostics: segment records only
                 }
-                nseg += __popcll(__builtin_amdgcn_ballot_w64(got));
+                nseg += NLOSGR_FCOUNT_ON ? 0u : (unsigned)__popcll(__builtin_amdgcn_ballot_w64(got));
                 const int ntake = min(nidle, qcount);
                 qhead = (qhead + ntake) & (kRQ - 1);
                 qcount -= ntake;
@@ -578,6 +585,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
             wave_sync();
             const bool win = act && owner[key] == (unsigned char)lane;
             wave_sync();
+            if (NLOSGR_FCOUNT_ON) {
+                npair += 1u;
+                nseg += (unsigned)__popcll(__builtin_amdgcn_ballot_w64(act));
+                nsamp += (unsigned)__popcll(__builtin_amdgcn_ballot_w64(win));   // every lane: / 64 on the host
+            }
             const int remw = win ? d.rem : 0;
             float* hb = hist + (win ? (QUAD ? (d.pos & ~(VW - 1)) : d.pos) : (QUAD ? padq : pad));
             float t = d.t;
@@ -2303,7 +2315,7 @@ void launch_fwd(const KArgs& ka, size_t shm, hipStream_t s) {
     // NLOSGR_FTAIL=0: masked forward drain at every cutoff (A/B and parity cross-check); netf takes the
     // TAIL drain where its backward does (c dT <= 1/64), so both see the same support
     const char* ftail = getenv("NLOSGR_FTAIL");
-    const bool tail = kCanTail && ka.opt.cutoff >= kTailCutoff && !ka.counts && !(ftail && ftail[0] == '0') &&
+    const bool tail = kCanTail && ka.opt.cutoff >= kTailCutoff && (!ka.counts || NLOSGR_FCOUNT_ON) && !(ftail && ftail[0] == '0') &&
                       (MODE != NLOSGR_MODE_NETF || ka.opt.c_deltaT <= kSmallX);
     // NLOSGR_FSWEEP=1: the window sweep instead of the lane-serial TAIL drain (experimental; A/B)
     const char* fsw = getenv("NLOSGR_FSWEEP");

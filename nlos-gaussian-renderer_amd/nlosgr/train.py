@@ -110,17 +110,18 @@ def allreduce_step(grads, loss4, n_total, group=None, async_op=False):
     return finish()
 
 
-def slab_order(mu, wall, slabs=16, cells=8):
+def slab_order(mu, wall, slabs=8, cells=4, size=None, size_buckets=0):
     """Permutation of the Gaussians for the backward: sorted by cell of a slabs x cells x cells grid over
     their bounding box, slab (the coordinate axis along which the Gaussians lie in front of the relay
     wall: the largest component of centroid(mu) - centroid(wall)) major, then the other two axes in
-    order.  The backward's workgroups own 64 consecutive Gaussians; spatially compact blocks have alike
-    candidate boxes and ray counts at every wall point (the block's enumeration and drain end together
-    instead of waiting for its largest pair) and share Gaussian-record cache lines: C3 backward 1136 ->
-    933 ms (scripts/order_ab.py; a Morton order gives 939, depth alone 976).  Any order gives the same
-    gradients up to fp32 summation order.  Rank-consistent: the ranks of a wall shard hold the same
-    Gaussians and their bands' centroids pick the same axis, so their permutations agree (the bucketed
-    all-reduce sums rows in this order)."""
+    order, and inside a cell by `size` (ascending; TrainStep passes the largest log-scale).  The
+    backward's workgroups own 64 consecutive Gaussians: spatially compact blocks of alike size have
+    alike candidate boxes and ray counts at every wall point, so the block's enumeration and drain end
+    together instead of waiting for its largest pair.  C3 backward (same box, scripts/env_ab.sh):
+    given order 951 ms, 16x8 cells 937, 8x4 cells + size 887; size-quantile-major buckets 911
+    (`size_buckets`).  Any order gives the same gradients up to fp32 summation order.
+    Rank-consistent: the ranks of a wall shard hold the same Gaussians and their bands' centroids
+    pick the same axis, so their permutations agree (the bucketed all-reduce sums rows in this order)."""
     with torch.no_grad():
         d = mu.mean(0) - wall.reshape(-1, 3).mean(0)
         k = int(torch.argmax(d.abs()))
@@ -130,7 +131,15 @@ def slab_order(mu, wall, slabs=16, cells=8):
         n = torch.tensor([slabs, cells, cells], device=mu.device, dtype=q.dtype)
         cell = ((q - lo) / (hi - lo).clamp_min(1e-12) * n).floor().clamp(max=n - 1).long()
         key = (cell[:, 0] * cells + cell[:, 1]) * cells + cell[:, 2]
-        return torch.argsort(key, stable=True)
+        if size is None:
+            return torch.argsort(key, stable=True)
+        if size_buckets:                                     # size-quantile bucket major, then cell
+            rank = torch.empty_like(key)
+            rank[torch.argsort(size, stable=True)] = torch.arange(key.numel(), device=key.device)
+            b = rank * size_buckets // key.numel()
+            return torch.argsort(b * (slabs * cells * cells) + key, stable=True)
+        by_size = torch.argsort(size, stable=True)          # within a cell: ascending size
+        return by_size[torch.argsort(key[by_size], stable=True)]
 
 
 def bucket_bounds(ng, nbuckets):
@@ -364,9 +373,12 @@ class TrainStep:
         # indexed by the forward's order); its gradients are scattered back below
         perm = None
         if self.bwd_order == "slab" and not cache and cfg.mode != "occl" and cfg.selection == "support" and ng > 64:
-            sl = os.environ.get("NLOSGR_SLAB")   # "slabs,cells" (A/B of the grid; default 16,8)
-            sc = tuple(int(v) for v in sl.split(",")) if sl else (16, 8)
-            perm = slab_order(args[0], self.geo.wall, *sc)
+            sl = os.environ.get("NLOSGR_SLAB")   # A/B knobs: "slabs,cells" (default 8,4); size key 0 = off,
+            sc = tuple(int(v) for v in sl.split(",")) if sl else (8, 4)   # 1 = max log-scale, 2 = log-volume
+            sz = os.environ.get("NLOSGR_SLAB_SIZE", "1")
+            size = args[1].max(1).values if sz == "1" else (args[1].sum(1) if sz == "2" else None)
+            perm = slab_order(args[0], self.geo.wall, *sc, size=size,
+                              size_buckets=int(os.environ.get("NLOSGR_SLAB_SIZEB", "0")))
             args = tuple(t[perm].contiguous() for t in args[:5]) + (args[5],)
 
         def unperm(gs):

@@ -17,11 +17,26 @@ def test_slab_order_permutation_and_bands():
     perm = slab_order(mu, walls)
     assert torch.equal(torch.sort(perm).values, torch.arange(5000))
     assert torch.equal(perm, slab_order(mu, walls))
-    # depth (y: the volume sits at y = 0.5 in front of the wall) is non-decreasing in 16 slabs
+    # depth (y: the volume sits at y = 0.5 in front of the wall) is non-decreasing in 8 slabs
     y = mu[perm, 1]
-    slab = ((y - y.min()) / (y.max() - y.min()) * 16).floor().clamp(max=15)
+    slab = ((y - y.min()) / (y.max() - y.min()) * 8).floor().clamp(max=7)
     assert bool((slab[1:] >= slab[:-1]).all())
+    # with a size key (TrainStep: the largest log-scale) the cells keep their order and each cell is
+    # sorted by size
+    size = m._scaling.detach().max(1).values
+    ps = slab_order(mu, walls, size=size)
+    assert torch.equal(torch.sort(ps).values, torch.arange(5000))
+    ys = mu[ps, 1]
+    slab_s = ((ys - y.min()) / (y.max() - y.min()) * 8).floor().clamp(max=7)
+    assert bool((slab_s[1:] >= slab_s[:-1]).all())
+    lo, hi = mu.min(0).values, mu.max(0).values
+    cell = ((mu - lo) / (hi - lo) * torch.tensor([4.0, 8.0, 4.0])).floor().clamp(max=torch.tensor([3.0, 7.0, 3.0]))
+    key = (cell[:, 1] * 4 + cell[:, 0]) * 4 + cell[:, 2]      # slab axis y, then x, z
+    ks, ss = key[ps], size[ps]
+    same = ks[1:] == ks[:-1]
+    assert bool((ks[1:] >= ks[:-1]).all()) and bool((ss[1:][same] >= ss[:-1][same]).all())
     for world in (2, 8):
         for r in range(world):
             band = walls[wall_rows(32, 32, r, world)]
             assert torch.equal(slab_order(mu, band), perm)
+            assert torch.equal(slab_order(mu, band, size=size), ps)
