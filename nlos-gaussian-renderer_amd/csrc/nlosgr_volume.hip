@@ -1452,7 +1452,7 @@ constexpr int kBSteps = NLOSGR_BSTEPS;   // bins per lane per backward drain rou
 #define NLOSGR_BSTEPS_NETF 16
 #endif
 #ifndef NLOSGR_BSTEPS_TAIL
-#define NLOSGR_BSTEPS_TAIL 32
+#define NLOSGR_BSTEPS_TAIL 40
 #endif
 // the staged gradient row is zero-padded by the longest round (no-occlusion TAIL rounds)
 constexpr int kBPad = NLOSGR_BSTEPS_TAIL > kBSteps ? NLOSGR_BSTEPS_TAIL : kBSteps;
