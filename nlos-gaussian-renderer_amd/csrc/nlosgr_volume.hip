@@ -1451,6 +1451,9 @@ constexpr int kBSteps = NLOSGR_BSTEPS;   // bins per lane per backward drain rou
 #ifndef NLOSGR_BSTEPS_NETF
 #define NLOSGR_BSTEPS_NETF 16
 #endif
+#ifndef NLOSGR_BPREFIX
+#define NLOSGR_BPREFIX 1   // no-occlusion culled backward: moments by nested running sums (see bwd_kernel)
+#endif
 #ifndef NLOSGR_BSTEPS_TAIL
 #define NLOSGR_BSTEPS_TAIL 40
 #endif
@@ -1611,8 +1614,20 @@ __device__ __forceinline__ bool bray_setup(const float* pd, float2 th, float2 ph
 // TAIL (culled no-occlusion histogram backward at cutoff >= kTailCutoff): the drain reads the upstream
 // row without the segment-end mask, see BV below
 
+#ifdef NLOSGR_BCOUNT
+// debug build (scripts/bwd_counts.py): loop iterations, drain rounds, active lanes, hand-off rounds,
+// pending lanes, hand-offs done, refills, rays taken (per wave, summed), read by nlosgr_debug_bwd_counts
+__device__ unsigned long long g_bdbg[8];
+#define BDBG(i, v) bdbg[i] += (unsigned long long)(v)
+#else
+#define BDBG(i, v) ((void)0)
+#endif
+
 template <int PRESET, int MODE, bool DENSE, bool RAYS, bool CACHE, bool SHR, bool TAIL = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) void bwd_kernel(KArgs k) {
+#ifdef NLOSGR_BCOUNT
+    unsigned long long bdbg[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
     // bins per drain round: netf keeps more per-ray state, so its rounds are shorter (no spill at 128 VGPRs)
     // (the no-occlusion TAIL rounds are longer: 32 bins measured 1137 vs 1170 ms at 24 on C3, and only
     // that variant stays spill-free at 32)
@@ -1780,6 +1795,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
                     if (MODE == NLOSGR_MODE_NETF && TAIL) b.T *= b.st;   // sin(theta) rides on T (BV rows)
                 }
                 const int ntake = min(nidle, qcount);
+                BDBG(6, 1); BDBG(7, ntake);
                 qhead = (qhead + ntake) & (kRQ - 1);
                 qcount -= ntake;
             }
@@ -1789,6 +1805,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
                 if (!anymore && qcount == 0) break;
                 continue;
             }
+            BDBG(0, 1);
+            if (anyact) { BDBG(1, 1); BDBG(2, __popcll(__builtin_amdgcn_ballot_w64(act))); }
             if (anyact) {
                 const int remw = act ? b.rem : 0;
                 // BV: the round starts at the even bin at or below pos (float2 row reads, half the LDS
@@ -1858,6 +1876,29 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
                         if (BV && TAIL && !(act && b.rem > 0)) pdf = 0.f;
                         float q = fast_exp2(b.c2 * fmaf(2.f, kap, 1.f));
                         const float cc = fast_exp2(2.f * b.c2);
+#if NLOSGR_BPREFIX
+                        // three nested running sums (one fma, two adds per bin): with w = kRS - m,
+                        // A = sum hp, B = sum hp w, C = sum hp w (w + 1) / 2, hp = H pdf; then about
+                        // K = kap at slot kRS: sum hp (K - w)^n for n = 0, 1, 2 (w^2 sums to 2C - B)
+                        float A = 0.f, B = 0.f, C = 0.f;
+#pragma unroll
+                        for (int m = 0; m < kRS; ++m) {
+                            A = fmaf(Hs[m], pdf, A);
+                            B += A;
+                            C += B;
+                            if (BV && m < BVW - 1) {   // the recurrence starts at pos (slot o)
+                                pdf = m < o ? pdf : pdf * q;
+                                q = m < o ? q : q * cc;
+                            } else {
+                                pdf *= q;
+                                q *= cc;
+                            }
+                        }
+                        const float K = kap - (float)o + (float)kRS;
+                        S0 += A;
+                        S1 += fmaf(K, A, -B);
+                        S2 += fmaf(K, fmaf(K, A, -2.f * B), fmaf(2.f, C, -B));
+#else
                         float U0 = 0.f, U1 = 0.f, U2 = 0.f;
 #pragma unroll
                         for (int m = 0; m < kRS; ++m) {
@@ -1877,6 +1918,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
                         S0 += U0;
                         S1 += fmaf(kb, U0, U1);
                         S2 += fmaf(kb, fmaf(kb, U0, 2.f * U1), U2);
+#endif
                         kap += (float)(kRS - o);
                     } else
 #pragma unroll
@@ -2069,6 +2111,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
                     dSig += gSig;
                     drho_pair += gRho;
                 }
+                BDBG(3, 1); BDBG(4, __popcll(pmask)); BDBG(5, __popcll(__builtin_amdgcn_ballot_w64(won)));
                 if (won) pend = false;
             }
         }
@@ -2091,6 +2134,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
         }
         if (active) k.drho[(size_t)(p - k.pb0) * k.g.ng + gio] = (wpair > 0.f && !(k.opt.flags & 64)) ? drho_pair : 0.f;
     }
+#ifdef NLOSGR_BCOUNT
+    if (lane == 0)
+        for (int c = 0; c < 8; ++c) atomicAdd(&g_bdbg[c], bdbg[c]);
+#endif
     if (shr) {   // shared layout: every wave owns its Gaussians for the whole split
         if (active) {
             // (rows of this split belong to this workgroup only; the first batch overwrites whatever the
@@ -2493,6 +2540,14 @@ int run_fwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_
 extern "C" {
 
 int nlosgr_abi_version(void) { return NLOSGR_ABI_VERSION; }
+
+#ifdef NLOSGR_BCOUNT
+__attribute__((visibility("default"))) int nlosgr_debug_bwd_counts(unsigned long long* out8) {
+    if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_bdbg), 8 * sizeof(unsigned long long)) != hipSuccess) return -1;
+    const unsigned long long zero[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_bdbg), zero, sizeof(zero)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 void nlosgr_set_batch_budgets(double drho_mb, double tile_hpart_mb) {
     BatchBudgets& b = batch_budgets();
