@@ -442,12 +442,31 @@ __device__ __forceinline__ void compiler_fence() { __asm__ __volatile__("" ::: "
 // Gaussian's peak (<= 3.7e-6 at m_c >= kTailCutoff), so the result lies between the culled and the
 // dense sum.  Bins past nr land in the zeroed pad row.
 constexpr float kTailCutoff = 5.0f;
+// Conveyor drain (TAIL no-occlusion float2 drain): lane l only ever holds a segment whose current bin
+// pair is = l + (kSteps / 2) R (mod 64) in drain round R.  Every active lane advances kSteps / 2 pairs per
+// round, so the invariant holds round after round, the 64 lanes always write 64 distinct pairs (no claim
+// table) and each 16-lane group of a ds_write_b64 (32-lane half of a ds_read_b64) covers 16 (32)
+// consecutive pairs: no bank conflicts.  A new segment is placed, at refill, in the free lane at or
+// below its residue's lane; a lane d below its own starts d pairs before its support (the Gaussian's
+// exact values there, as past its end; only while the seed stays >= 2^-120).  Placement: up to
+// kPlaceIters rounds of forward-permute claims on free lanes, then the winners' drain state moves by
+// bpermute; segments left unplaced go back to the head of the ray queue.  0 = claim-table drain.
+#ifndef NLOSGR_FCONV
+#define NLOSGR_FCONV 0
+#endif
+constexpr bool kFConv = NLOSGR_FCONV != 0;
+#ifndef NLOSGR_PLACE_ITERS
+#define NLOSGR_PLACE_ITERS 3
+#endif
+constexpr int kPlaceIters = NLOSGR_PLACE_ITERS;
 // debug build (-DNLOSGR_FCOUNT, scripts/drain_counts.py): count_support runs the TAIL forward and returns
 // (wave drain rounds, active lanes summed over rounds, claim winners summed) instead of its work counts
 #ifdef NLOSGR_FCOUNT
 #define NLOSGR_FCOUNT_ON 1
+#define NLOSGR_FCOUNT_MODE (NLOSGR_FCOUNT + 0)   // 2: conveyor placement (refills, leftovers, shift pairs)
 #else
 #define NLOSGR_FCOUNT_ON 0
+#define NLOSGR_FCOUNT_MODE 0
 #endif
 constexpr float kBetaSeries = 0.5f;   // bin-integrated TAIL drain: series bin average up to this beta
 
@@ -503,6 +522,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
     d.wrap = 0; d.tw = 0.f;
     bool act = false;
     int qhead = 0, qcount = 0;
+    unsigned conv_r = 0;   // conveyor: drain rounds so far (wave-uniform)
 
     for (int base = g_lo + wave * 64;; base += kBlock) {
         const bool have = base < g_hi;         // wave-uniform
@@ -570,6 +590,76 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
                 const int ntake = min(nidle, qcount);
                 qhead = (qhead + ntake) & (kRQ - 1);
                 qcount -= ntake;
+                if (kFConv && QUADF && TAIL && MODE == NLOSGR_MODE_NOOCL) {
+                    // place this refill's segments (lanes `take && act`) on free lanes of their residue
+                    const bool newl = take && act;
+                    unsigned long long avail = __builtin_amdgcn_ballot_w64(!act || take);   // no old segment
+                    const int k0 = d.pos >> 1, o = d.pos & 1;
+                    const int r0 = (k0 - (int)(conv_r * (unsigned)(kSteps / 2))) & 63;
+                    // pairs the start may move down: the seed at bin 2 (k0 - s) keeps d.ga t^2 + d.al >= -120
+                    const float span = d.al + 120.f;
+                    const float tm = span > 0.f ? sqrtf(span / fmaxf(-d.ga, 1e-30f)) : 0.f;
+                    const int smax = newl ? min(k0, (int)floorf(0.5f * (d.t - (float)o + tm))) : 0;
+                    bool unpl = newl, placed = false;
+                    int src = lane, dsh = 0;
+                    bool recv_any = false;
+#pragma unroll
+                    for (int itp = 0; itp < kPlaceIters; ++itp) {
+                        if (!__builtin_amdgcn_ballot_w64(unpl)) break;
+                        const int sr = 63 - r0;   // rotate: bit 63 <-> lane r0, bit 63 - s <-> lane r0 - s
+                        const unsigned long long x = sr ? ((avail << sr) | (avail >> (64 - sr))) : avail;
+                        const int dl = x ? (int)__builtin_clzll(x) : 64;
+                        const bool can = unpl && dl <= max(smax, 0) && dl < 64;
+                        const int tg = (r0 - dl) & 63;
+                        // forward-permute claim (highest sender wins a lane; see the backward hand-off)
+                        const int pv = can ? lane + 1 : 0;
+                        const int w1 = __builtin_amdgcn_ds_permute((can ? tg : 0) << 2, pv);
+                        const int w2 = __builtin_amdgcn_ds_permute((can ? tg : 1) << 2, pv);
+                        const int wcl = lane == 0 ? w2 : w1;
+                        const int back = __builtin_amdgcn_ds_bpermute(tg << 2, wcl);
+                        const bool won = can && back == lane + 1;
+                        if (wcl != 0) { src = wcl - 1; recv_any = true; }
+                        if (won) { placed = true; dsh = dl; }
+                        if (won || !can) unpl = false;   // !can: nothing free within reach -> back to the queue
+                        avail &= ~__builtin_amdgcn_ballot_w64(wcl != 0);
+                    }
+                    const bool leftover = newl && !placed;
+                    if (NLOSGR_FCOUNT_MODE == 2) {
+                        npair += 1u;
+                        nseg += (unsigned)__popcll(__builtin_amdgcn_ballot_w64(leftover));
+                        nsamp += placed ? (unsigned)dsh : 0u;
+                    }
+                    // placed segments start dsh pairs lower (dsh > 0: at the even bin, seeded there)
+                    int npos = d.pos, nrem = d.rem;
+                    float nt_ = d.t;
+                    if (placed && dsh > 0) {
+                        npos = 2 * (k0 - dsh);
+                        nrem = d.rem + o + 2 * dsh;
+                        nt_ = d.t - (float)(o + 2 * dsh);
+                    }
+                    // move: every lane reads its source lane's state (its own when it received nothing)
+                    const int sa = src << 2;
+                    const int mpos = __builtin_amdgcn_ds_bpermute(sa, npos);
+                    const int mrem = __builtin_amdgcn_ds_bpermute(sa, nrem);
+                    const float mt = __int_as_float(__builtin_amdgcn_ds_bpermute(sa, __float_as_int(nt_)));
+                    const float mga = __int_as_float(__builtin_amdgcn_ds_bpermute(sa, __float_as_int(d.ga)));
+                    const float mal = __int_as_float(__builtin_amdgcn_ds_bpermute(sa, __float_as_int(d.al)));
+                    if (recv_any) {
+                        d.pos = mpos; d.rem = mrem; d.t = mt; d.ga = mga; d.al = mal;
+                        act = true;
+                    } else if (newl) {
+                        act = false;   // its segment moved out, or goes back to the queue
+                    }
+                    // unplaced segments: their queue entries back to the head of the ring
+                    const unsigned long long lm = __builtin_amdgcn_ballot_w64(leftover);
+                    if (lm) {
+                        const int nl = __popcll(lm);
+                        qhead = (qhead - nl) & (kRQ - 1);
+                        if (leftover) rayq[(qhead + lanes_below(lm)) & (kRQ - 1)] = e;
+                        qcount += nl;
+                        wave_sync();
+                    }
+                }
             }
             const bool anyact = __builtin_amdgcn_ballot_w64(act) != 0;
             if (!anyact) {
@@ -580,12 +670,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
             // claim distinct start keys (distinct addresses; vector drain: distinct start pairs)
             constexpr bool QUAD = QUADF;
             constexpr int VW = 2;   // bins per LDS read-add-write of the vector drain (float2)
-            const int key = QUAD ? (d.pos / VW) : d.pos;
-            if (act) owner[key] = (unsigned char)lane;
-            wave_sync();
-            const bool win = act && owner[key] == (unsigned char)lane;
-            wave_sync();
-            if (NLOSGR_FCOUNT_ON) {
+            constexpr bool CONV = kFConv && QUADF && TAIL && MODE == NLOSGR_MODE_NOOCL;
+            bool win = act;   // conveyor: distinct pairs by construction
+            if (!CONV) {
+                const int key = QUAD ? (d.pos / VW) : d.pos;
+                if (act) owner[key] = (unsigned char)lane;
+                wave_sync();
+                win = act && owner[key] == (unsigned char)lane;
+                wave_sync();
+            }
+            if (NLOSGR_FCOUNT_ON && NLOSGR_FCOUNT_MODE != 2) {
                 npair += 1u;
                 nseg += (unsigned)__popcll(__builtin_amdgcn_ballot_w64(act));
                 nsamp += (unsigned)__popcll(__builtin_amdgcn_ballot_w64(win));   // every lane: / 64 on the host
@@ -812,6 +906,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
                 }
                 act = d.rem > 0;
             }
+            if (CONV) ++conv_r;
         }
         if (CACHE && have && base + lane < g_hi) {
             // every candidate of this chunk has been tested: record the pair's passing cells
