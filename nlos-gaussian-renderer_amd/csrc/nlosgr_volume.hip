@@ -459,6 +459,10 @@ constexpr bool kFConv = NLOSGR_FCONV != 0;
 #define NLOSGR_PLACE_ITERS 3
 #endif
 constexpr int kPlaceIters = NLOSGR_PLACE_ITERS;
+#ifndef NLOSGR_PLACE_SPREAD
+#define NLOSGR_PLACE_SPREAD 8
+#endif
+constexpr int kPlaceSpread = NLOSGR_PLACE_SPREAD;   // power of two
 // debug build (-DNLOSGR_FCOUNT, scripts/drain_counts.py): count_support runs the TAIL forward and returns
 // (wave drain rounds, active lanes summed over rounds, claim winners summed) instead of its work counts
 #ifdef NLOSGR_FCOUNT
@@ -605,10 +609,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
                     bool recv_any = false;
 #pragma unroll
                     for (int itp = 0; itp < kPlaceIters; ++itp) {
-                        if (!__builtin_amdgcn_ballot_w64(unpl)) break;
-                        const int sr = 63 - r0;   // rotate: bit 63 <-> lane r0, bit 63 - s <-> lane r0 - s
+                        const unsigned long long um = __builtin_amdgcn_ballot_w64(unpl);
+                        if (!um) break;
+                        // segments of one pair start on the same residue: spread the senders over the
+                        // kPlaceSpread lanes below it by their rank, then take the nearest free lane below
+                        const int j0 = (lanes_below(um) + 3 * itp) & (kPlaceSpread - 1);
+                        const int rs = (r0 - j0) & 63;
+                        const int sr = 63 - rs;   // rotate: bit 63 <-> lane rs, bit 63 - s <-> lane rs - s
                         const unsigned long long x = sr ? ((avail << sr) | (avail >> (64 - sr))) : avail;
-                        const int dl = x ? (int)__builtin_clzll(x) : 64;
+                        const int dl = x ? (int)__builtin_clzll(x) + j0 : 64;
                         const bool can = unpl && dl <= max(smax, 0) && dl < 64;
                         const int tg = (r0 - dl) & 63;
                         // forward-permute claim (highest sender wins a lane; see the backward hand-off)
