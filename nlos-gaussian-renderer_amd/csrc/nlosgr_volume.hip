@@ -2063,6 +2063,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
                         // A's weight is c rho H_j T_j - P_j a_c = crho HT + k1 drho; sum_j c1_j pdf_j (dsigma's
                         // part A) is UA0, summed per round below
                         const float k1 = -b.rho * ac;
+                        // part A's moments by nested running sums (as the no-occlusion drain): UA0 = sum hA,
+                        // UA1 = sum hA w, UA2 = sum hA w (w + 1) / 2 with w = kRS - m; part B's directly
                         float UA0 = 0.f, UA1 = 0.f, UA2 = 0.f, UB0 = 0.f, UB1 = 0.f, UB2 = 0.f;
 #pragma unroll
                         for (int m = 0; m < kRS; ++m) {
@@ -2081,10 +2083,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
                             drho += hdt;
                             const float c1 = in ? fmaf(k1, drho, crho * HT) : 0.f;
                             const float pin = in ? pdf : 0.f;
-                            const float hA = c1 * pdf;                // x sigma at the end
-                            UA0 += hA;
-                            UA1 = fmaf(hA, (float)m, UA1);
-                            UA2 = fmaf(hA, (float)(m * m), UA2);
+                            UA0 = fmaf(c1, pdf, UA0);                 // x sigma at the end
+                            UA1 += UA0;
+                            UA2 += UA1;
                             UB0 += pin;
                             UB1 = fmaf(pin, (float)m, UB1);
                             UB2 = fmaf(pin, (float)(m * m), UB2);
@@ -2095,9 +2096,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
                         // S_n += sum h (kb + m)^n, kb = the round's first bin offset
                         const float kb = kseed;
                         const float sg = b.sigma, sgb = b.sigma * ac;
+                        const float KA = kb + (float)kRS;   // kap at slot kRS
                         S0 = fmaf(sg, UA0, S0);
-                        S1 = fmaf(sg, fmaf(kb, UA0, UA1), S1);
-                        S2 = fmaf(sg, fmaf(kb, fmaf(kb, UA0, 2.f * UA1), UA2), S2);
+                        S1 = fmaf(sg, fmaf(KA, UA0, -UA1), S1);
+                        S2 = fmaf(sg, fmaf(KA, fmaf(KA, UA0, -2.f * UA1), fmaf(2.f, UA2, -UA1)), S2);
                         S0b = fmaf(sgb, UB0, S0b);
                         S1b = fmaf(sgb, fmaf(kb, UB0, UB1), S1b);
                         S2b = fmaf(sgb, fmaf(kb, fmaf(kb, UB0, 2.f * UB1), UB2), S2b);
