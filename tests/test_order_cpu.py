@@ -40,3 +40,20 @@ def test_slab_order_permutation_and_bands():
             band = walls[wall_rows(32, 32, r, world)]
             assert torch.equal(slab_order(mu, band), perm)
             assert torch.equal(slab_order(mu, band, size=size), ps)
+
+
+def test_forward_order_slabs_by_size():
+    """The forward's order (TrainStep fwd_order="slab"): 8 depth slabs, each sorted by size."""
+    from nlosgr.geometry import relay_wall_grid
+    from nlosgr.model import GaussianParams
+    from nlosgr.train import slab_order
+    m = GaussianParams.synthetic(3000, 3, preset="cuda", device="cpu", seed=9)
+    mu, size = m._mu.detach(), m._scaling.detach().max(1).values
+    perm = slab_order(mu, relay_wall_grid(16, 16), 8, 1, size=size)
+    assert torch.equal(torch.sort(perm).values, torch.arange(3000))
+    y = mu[:, 1]
+    slab = ((y - y.min()) / (y.max() - y.min()) * 8).floor().clamp(max=7)[perm]
+    assert bool((slab[1:] >= slab[:-1]).all())
+    s = size[perm]
+    same = slab[1:] == slab[:-1]
+    assert bool((s[1:][same] >= s[:-1][same]).all())
