@@ -138,19 +138,54 @@ def committed_profile(cfg_name, kind, cutoff, preset="cuda", mode="noocl", selec
     return None, None
 
 
-def pmc_traffic(cfg_name, kernels, cutoff, **wl):
-    """HBM bytes per launch of `kernels` (name substrings): FETCH_SIZE x2 + WRITE_SIZE passes
-    (MI355X_MICROARCH.md §HBM), from the committed traffic profile of the same workload, or None."""
+# the kernels each timed phase launches (families: the kernel's name without template arguments);
+# preprocess_kernel runs once in each phase
+PHASE_KERNELS = {
+    "fwd": ("preprocess_kernel", "fx_amax_kernel", "fwd_kernel", "fwd_dense_kernel", "fx_reduce_kernel",
+            "hist_reduce_kernel"),
+    "bwd": ("preprocess_kernel", "bwd_kernel", "sh_kernel", "finish_kernel"),
+    "tiles_fwd": ("preprocess_kernel", "tile_kernel", "tiles_reduce_kernel"),
+    "tiles_bwd": ("preprocess_kernel", "tile_kernel", "tiles_finish_kernel"),
+}
+SHARED_KERNELS = ("preprocess_kernel",)
+
+
+def kernel_family(name):
+    """'void fwd_kernel<1, 0, ...>' -> 'fwd_kernel' (the traffic profiles' short names)."""
+    n = name[5:] if name.startswith("void ") else name
+    return n.split("<", 1)[0].strip()
+
+
+def phase_traffic(kernels, phase):
+    """HBM bytes per step of one timed phase from a traffic profile's per-kernel records: every kernel
+    of the phase's families that runs every step (launches_per_step >= 0.5: the untimed support-count
+    launch runs once per run and is left out), each at its launches per step (a kernel of both phases
+    counts one launch per phase); the ray-tile engine's tile_kernel<SEL, DENSE, OCCL, BWD> is split by
+    its BWD argument.  Returns (bytes, [kernel names]) or (None, [])."""
+    fams = PHASE_KERNELS[phase]
+    total, used = 0.0, []
+    for k, v in kernels.items():
+        fam = kernel_family(k)
+        if fam not in fams or v.get("launches_per_step", 1.0) < 0.5:
+            continue
+        if fam == "tile_kernel" and k.rstrip().endswith("true>") != (phase == "tiles_bwd"):
+            continue
+        per = v["hbm_bytes_per_launch"]
+        total += per if fam in SHARED_KERNELS else per * v.get("launches_per_step", 1.0)
+        used.append(k)
+    return (total, used) if used else (None, [])
+
+
+def pmc_traffic(cfg_name, cutoff, tiles, **wl):
+    """HBM bytes per step of the forward and backward phases: FETCH_SIZE x2 + WRITE_SIZE passes
+    (MI355X_MICROARCH.md §HBM) from the committed traffic profile of the same workload, or Nones."""
     rec, src = committed_profile(cfg_name, "traffic", cutoff, **wl)
     if rec is None:
-        return None, None
-    total = 0.0
-    for sub in kernels:
-        hits = [v.get("hbm_bytes_per_step", v["hbm_bytes_per_launch"]) for k, v in rec["kernels"].items() if sub in k]
-        if not hits:
-            return None, None
-        total += max(hits)
-    return total, src
+        return {"fwd": None, "bwd": None}, None
+    out = {}
+    for ph in ("fwd", "bwd"):
+        out[ph] = phase_traffic(rec["kernels"], ("tiles_" + ph) if tiles else ph)[0]
+    return out, src
 
 
 class Snapshot:
@@ -441,15 +476,14 @@ def main():
     tiles = a.mode == "occl" or a.selection == "aabb"     # ray-tile engine (csrc/nlosgr_tiles.hip)
     if bwd_avg >= fwd_avg:
         dom, dom_ms, dom_bytes = "bwd", bwd_avg, 2 * ng * pb + V
-        kern = (("preprocess_kernel", "tile_kernel", "tiles_finish_kernel") if tiles else
-                ("preprocess_kernel", "bwd_kernel", "sh_kernel", "finish_kernel"))
     else:
         dom, dom_ms, dom_bytes = "fwd", fwd_avg, ng * pb + V
-        kern = ("preprocess_kernel", "tile_kernel", "tiles_reduce_kernel") if tiles else ("preprocess_kernel", "fwd_kernel")
+    kern = PHASE_KERNELS[("tiles_" + dom) if tiles else dom]
     wl = {"preset": a.preset, "mode": a.mode, "selection": a.selection}
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
     single = a.band <= 1 and world == 1
-    traffic, traffic_src = pmc_traffic(a.config, kern, a.cutoff, **wl) if single else (None, None)
+    phase_tr, traffic_src = pmc_traffic(a.config, a.cutoff, tiles, **wl) if single else ({"fwd": None, "bwd": None}, None)
+    traffic = phase_tr[dom]
     # compute-side figures: exact in-support evaluations of the (frozen) workload per second, and the
     # VALU issue utilisation from the committed SQ counter pass of this command
     # (SQ_INSTS_VALU x 2 cycles per wave64 instruction / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs); the 2
@@ -488,6 +522,8 @@ def main():
         "roofline": {"bound": "hbm", "kernel": f"nlosgr {dom} ({' + '.join(kern)})", "achieved": achieved,
                      "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS,
                      "traffic": traffic, "traffic_source": traffic_src,
+                     "traffic_per_phase": {"fwd": phase_tr["fwd"], "bwd": phase_tr["bwd"],
+                                           "unit": "HBM bytes per step (PMC FETCH_SIZE x2 + WRITE_SIZE)"},
                      "algorithmic_bytes_per_launch": dom_bytes, "avg_launch_ms": dom_ms},
         "compute": valu,
     }

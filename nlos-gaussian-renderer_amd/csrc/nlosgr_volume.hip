@@ -75,6 +75,8 @@ struct KArgs {
     int pb0, pnw;                // backward: wall points [pb0, pb0 + pnw) of this launch (a batch; drho rows
                                  // are indexed p - pb0, so the dL/drho buffer holds one batch, not the wall)
     int accum;                   // backward batches after the first add into the partial slabs
+    unsigned long long* hfx;     // forward FX drain: fixed-point histogram [P][nr] (u64, integer adds)
+    const unsigned* fx_amax;     // forward FX drain: bits of the launch's amplitude bound (fx_amax_kernel)
 };
 
 // ray cache: a pair whose (theta, phi) candidate box has at most 128 cells records which cells
@@ -474,11 +476,43 @@ constexpr int kPlaceSpread = NLOSGR_PLACE_SPREAD;   // power of two
 #endif
 constexpr float kBetaSeries = 0.5f;   // bin-integrated TAIL drain: series bin average up to this beta
 
-template <int PRESET, int MODE, bool DENSE, bool RAYS, bool CACHE, bool TAIL = false>
+// Fixed-point drain (FX; TAIL no-occlusion histogram, the training hot path).  The wave's LDS histogram
+// holds each bin as an unsigned 32-bit count of units 2^-E; a round adds two bins per lane with ONE
+// no-return ds_add_u64 of the packed pair (low word = even bin, high word = odd bin), so no claim table:
+// every active lane drains every round, and integer adds make the sum independent of the order (the
+// forward is bitwise deterministic whatever the schedule).  E is set per launch so that the launch's
+// amplitude bound (max over Gaussians of sigma * rho_max, fx_amax_kernel) is < 2^kFxBits units; a
+// value rounds to the nearest unit (v_cvt_rpi_i32_f32), i.e. the absolute error per term is <= 2^-(kFxBits+1)
+// of the brightest possible term.  A low word must never carry into its high word: every lane sums the
+// peaks (exp2 of the segment's log2 amplitude, in units) of the segments it took since the last check;
+// a segment adds at most its peak to any bin once, so while every lane's sum stays <= thr the largest
+// field stays <= M + 64 thr < 2^32.  When a lane passes thr the wave reads its histogram's true maximum
+// M; past 2^31 it moves the fields into the u64 histogram in global memory (integer atomics; rare) and
+// zeroes them.  At the end each workgroup adds its 4 waves' fields to the global u64 histogram [P][nr]
+// (all Gaussian splits of a wall point meet there), and fx_reduce_kernel scales it to floats.
+constexpr int kFxBits = 24;
+constexpr float kFxLimit = 4294967040.0f;   // largest float below 2^32
+__device__ __forceinline__ int fx_exponent(unsigned amax_bits) {
+    const float a = __uint_as_float(amax_bits);
+    if (!(a > 0.f) || !(a < 3.0e38f)) return 0;
+    int e;
+    frexpf(a, &e);   // a < 2^e
+    e = kFxBits - e;
+    return e < -120 ? -120 : (e > 120 ? 120 : e);
+}
+// round to nearest (floor(x + 0.5)) as an integer in one VALU instruction; 0 <= x < 2^31
+__device__ __forceinline__ unsigned cvt_rpi(float x) {
+    int r;
+    __asm__("v_cvt_rpi_i32_f32 %0, %1" : "=v"(r) : "v"(x));
+    return (unsigned)r;
+}
+
+template <int PRESET, int MODE, bool DENSE, bool RAYS, bool CACHE, bool TAIL = false, bool FX = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) void fwd_kernel(KArgs k) {
     extern __shared__ __align__(16) float smem[];
     const int nr = k.geo.nr, nt = k.geo.nt, np_ = k.geo.np;
     const FwdLayout L(nr, nt, np_);
+    static_assert(!FX || (TAIL && MODE == NLOSGR_MODE_NOOCL && !DENSE && !RAYS), "fixed-point drain: TAIL no-occlusion histogram");
     float2* tth = reinterpret_cast<float2*>(smem);
     float2* tph = tth + nt;
     const int wave = threadIdx.x >> 6, lane = lane_id();
@@ -511,6 +545,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
     float* rout = RAYS ? k.ray_out + (size_t)p * nt * np_ * nr : nullptr;
     const float rscale = k.opt.ray_scale;
     const int flags = k.opt.flags;
+    // FX: log2 of the unit scale, folded into every pair's log2 amplitude; per-lane peak bookkeeping
+    const float fxE = FX ? (float)fx_exponent(*k.fx_amax) : 0.f;
+    float fthr = kFxLimit / 64.f;   // wave-uniform
+    float fpk = 0.f, fxs = 0.f;     // this lane's segment peak, and its peaks since the last check
+    unsigned* hist32 = reinterpret_cast<unsigned*>(hist);
+    const int nfx = nr + kSteps + 2;   // fields a round can reach (bins past nr are pad)
     // the float2 drain (two bins per LDS read-add-write; claim keys on bin pairs)
     constexpr bool QUADF = (MODE == NLOSGR_MODE_NOOCL || ((MODE == NLOSGR_MODE_NETF || MODE == NLOSGR_MODE_BININT) && TAIL)) &&
                            !RAYS && !DENSE;
@@ -548,7 +588,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
                 load_rec(nrec, P, mu);
                 pair_setup<PRESET, DENSE>(k, k.g.features + (size_t)gl * k.g.k_feat, mu, px, py, pz, lin, mc2, P);
                 more = (P.w > 0.f) && P.i0 <= P.i1 && P.j0 <= P.j1;
-                lw = more ? flog2(P.w) : 0.f;
+                lw = more ? flog2(P.w) + fxE : 0.f;
                 sc = P.sigma * cdt;
                 wc = more ? P.w * cdt : 0.f;
             }
@@ -589,6 +629,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
                     if (got && !NLOSGR_FCOUNT_ON) nsamp += (unsigned)(d.rem + (dense_wrap<MODE, DENSE>() ? d.wrap : 0));
                     if (MODE == NLOSGR_MODE_NETF && TAIL && QUADF) d.T *= d.wc;   // the weight rides on T
                     act = got && !(flags & 4);    // diagnostics: segment records only
+                    if (FX && act) {
+                        fpk = fast_exp2(d.al);    // the segment's largest value (t = 0), in units
+                        fxs += fpk;
+                    }
                 }
                 nseg += NLOSGR_FCOUNT_ON ? 0u : (unsigned)__popcll(__builtin_amdgcn_ballot_w64(got));
                 const int ntake = min(nidle, qcount);
@@ -680,8 +724,29 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
             constexpr bool QUAD = QUADF;
             constexpr int VW = 2;   // bins per LDS read-add-write of the vector drain (float2)
             constexpr bool CONV = kFConv && QUADF && TAIL && MODE == NLOSGR_MODE_NOOCL;
-            bool win = act;   // conveyor: distinct pairs by construction
-            if (!CONV) {
+            bool win = act;   // conveyor: distinct pairs by construction; FX: integer adds, no claims
+            if (FX && __builtin_amdgcn_ballot_w64(fxs > fthr)) {
+                // a lane passed its share of the headroom: read the fields' true maximum (and move
+                // them to the global u64 histogram once it passes 2^31)
+                wave_sync();
+                unsigned mx = 0u;
+                for (int t = lane; t < nfx; t += 64) mx = max(mx, hist32[t]);
+                for (int o2 = 32; o2 > 0; o2 >>= 1) mx = max(mx, (unsigned)__shfl_xor((int)mx, o2));
+                if (mx >= 0x80000000u) {
+                    for (int t = lane; t < nfx; t += 64) {
+                        const unsigned v = hist32[t];
+                        if (v && t < nr)
+                            __hip_atomic_fetch_add(k.hfx + (size_t)p * nr + t, (unsigned long long)v, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT);
+                        hist32[t] = 0u;
+                    }
+                    wave_sync();
+                    mx = 0u;
+                }
+                fthr = (kFxLimit - (float)mx) * (1.0f / 64.0f);
+                fxs = act ? fpk : 0.f;   // an active segment may still add up to its peak to any bin
+            }
+            if (!CONV && !FX) {
                 const int key = QUAD ? (d.pos / VW) : d.pos;
                 if (act) owner[key] = (unsigned char)lane;
                 wave_sync();
@@ -706,7 +771,29 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
                 // per-step mask switching).
                 const int o = d.pos & (VW - 1);
                 const int lim = remw + o;   // slot j is in the segment iff o <= j < lim
-                if (TAIL && win && MODE == NLOSGR_MODE_NOOCL) {
+                if (FX && win) {
+                    // fixed point: the same values as below, rounded to units, two bins per ds_add_u64
+                    float cur = fast_exp2(fmaf(d.ga, t * t, d.al));
+                    float q = fast_exp2(d.ga * fmaf(2.f, t, 1.f));
+                    const float cc = fast_exp2(2.f * d.ga);
+                    unsigned long long* hb8 = reinterpret_cast<unsigned long long*>(hb);
+#pragma unroll
+                    for (int kv = 0; kv < kSteps / VW; ++kv) {
+                        const float v0 = (kv == 0 && o) ? 0.f : cur;
+                        if (kv == 0) {
+                            cur = o ? cur : cur * q;
+                            q = o ? q : q * cc;
+                        } else {
+                            cur *= q;
+                            q *= cc;
+                        }
+                        const float v1 = cur;
+                        cur *= q;
+                        q *= cc;
+                        const unsigned long long pv = ((unsigned long long)cvt_rpi(v1) << 32) | cvt_rpi(v0);
+                        __hip_atomic_fetch_add(hb8 + kv, pv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+                    }
+                } else if (TAIL && win && MODE == NLOSGR_MODE_NOOCL) {
                     // the recurrence is seeded at pos (inside the support: a seed one bin further out can
                     // underflow for Gaussians much narrower than a bin); slot 0 before pos (o = 1) adds 0
                     float cur = fast_exp2(fmaf(d.ga, t * t, d.al));
@@ -939,7 +1026,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
         }
     }
     __syncthreads();
-    if (k.hist_out) {
+    if (FX) {
+        // the 4 waves' fields of each bin -> one integer add into the wall point's global u64 row
+        for (int t = threadIdx.x; t < nr; t += blockDim.x) {
+            unsigned long long s = 0ull;
+            for (int w = 0; w < kWaves; ++w)
+                s += reinterpret_cast<const unsigned*>(smem + w * L.wave_stride + L.hist)[t];
+            if (s) __hip_atomic_fetch_add(k.hfx + (size_t)p * nr + t, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    } else if (k.hist_out) {
         const float hs = k.geo.hscale[p];
         for (int t = threadIdx.x; t < nr; t += blockDim.x) {
             float s = 0.f;
@@ -963,6 +1058,44 @@ __global__ __launch_bounds__(kBlock) void hist_reduce_kernel(const float* __rest
     float s = 0.f;
     for (int sp = 0; sp < nsp; ++sp) s += hpart[(size_t)sp * P * nr + i];
     hist[i] = s * att[t] * hscale[p];
+}
+
+// FX: the launch's amplitude bound max_g sigma_g * rho_max_g, rho_max = 0.5 + sum_l |f_l| sqrt((2l+1)/4pi)
+// (Cauchy-Schwarz with sum_m Y_lm(d)^2 = (2l+1)/4pi on the unit sphere; 5 % margin for the cuda preset's
+// eps-shortened view direction), as float bits (non-negative floats order like their bits)
+template <int PRESET>
+__global__ __launch_bounds__(kBlock) void fx_amax_kernel(nlosgr_gaussians g, unsigned* amax) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    float a = 0.f;
+    if (i < g.ng) {
+        const float sig = 1.0f / (1.0f + expf(-g.opacity[i]));
+        const float* f = g.features + (size_t)i * g.k_feat;
+        const int deg = min(g.sh_degree, PRESET == NLOSGR_PRESET_TORCH ? 4 : 3);
+        float sh = 0.f;
+        for (int l = 0; l <= deg; ++l) {
+            float n2 = 0.f;
+            for (int c = l * l; c < (l + 1) * (l + 1) && c < g.k_feat; ++c) n2 += f[c] * f[c];
+            sh += sqrtf(n2) * sqrtf((2.0f * l + 1.0f) * (0.25f / kPi));
+        }
+        a = sig * (0.5f + 1.05f * sh) * 1.001f;
+        if (!(a >= 0.f)) a = __uint_as_float(0x7f800000u);   // NaN parameters: E = 0
+    }
+    unsigned b = __float_as_uint(a);
+    for (int o = 32; o > 0; o >>= 1) b = max(b, (unsigned)__shfl_xor((int)b, o));
+    if (lane_id() == 0) atomicMax(amax, b);
+}
+
+// FX: hist[p,t] = (u64 count x 2^-E) x att[t] x hscale[p]
+__global__ __launch_bounds__(kBlock) void fx_reduce_kernel(const unsigned long long* __restrict__ hfx,
+                                                           const unsigned* __restrict__ amax, long long P, int nr,
+                                                           const float* __restrict__ att,
+                                                           const float* __restrict__ hscale, float* __restrict__ hist) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P * nr) return;
+    const long long p = i / nr;
+    const int t = (int)(i - p * nr);
+    const double q = ldexp(1.0, -fx_exponent(*amax));
+    hist[i] = (float)((double)hfx[i] * q) * att[t] * hscale[p];
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1428,8 +1561,8 @@ struct FwdDenseLayout {
     __host__ __device__ FwdDenseLayout(int nr, int nt, int np_) {
         const int off = al4(2 * (nt + np_));
         rays = off;                     // float4 [kWaves][64] (gamma, alpha, ks, -)
-        hist = rays + kWaves * 64 * 4;  // [kWaves][nr]
-        total = hist + kWaves * nr;
+        hist = rays + kWaves * 64 * 4;  // double [kWaves][nr]
+        total = hist + kWaves * nr * 2;
     }
 };
 
@@ -1458,9 +1591,16 @@ __global__ __launch_bounds__(kBlock) void fwd_dense_kernel(KArgs k) {
     const float dr = nr > 1 ? (k.geo.r[nr - 1] - r0) / (float)(nr - 1) : 0.f;
     const float inv_dr = dr > 0.f ? 1.0f / dr : 0.f;
     const int nray = nt * np_;
-    float acc[NB], kf[NB];
+    // each 64-ray batch's terms are summed in fp32 registers (<= 64 terms per bin) and folded into the
+    // lane's own bins of a wave-private fp64 histogram: a running fp32 total over every (Gaussian, ray)
+    // drops the terms below half an ulp of the bin (C2: 1.9e-5 low against float64)
+    double* wh = reinterpret_cast<double*>(smem + L.hist) + wave * nr;
+    float kf[NB];
 #pragma unroll
-    for (int b = 0; b < NB; ++b) { acc[b] = 0.f; kf[b] = (float)(lane + 64 * b); }
+    for (int b = 0; b < NB; ++b) {
+        kf[b] = (float)(lane + 64 * b);
+        if (lane + 64 * b < nr) wh[lane + 64 * b] = 0.0;
+    }
 
     for (int base = g_lo + wave * 64; base < g_hi; base += kBlock) {
         const int gi = base + lane;
@@ -1498,6 +1638,9 @@ __global__ __launch_bounds__(kBlock) void fwd_dense_kernel(KArgs k) {
                 rp[lane] = make_float4(ga, al, R.ks, 0.f);
                 wave_sync();
                 const int nq = min(64, nray - rb);
+                float acc[NB];
+#pragma unroll
+                for (int b = 0; b < NB; ++b) acc[b] = 0.f;
                 int q = 0;
                 for (; q + 4 <= nq; q += 4) {
                     float4 e[4];
@@ -1519,18 +1662,19 @@ __global__ __launch_bounds__(kBlock) void fwd_dense_kernel(KArgs k) {
                         acc[b] += fast_exp2(fmaf(e.x, t * t, e.y));
                     }
                 }
+#pragma unroll
+                for (int b = 0; b < NB; ++b)
+                    if (lane + 64 * b < nr) wh[lane + 64 * b] += (double)acc[b];
             }
         }
     }
-    float* wh = smem + L.hist + wave * nr;
-#pragma unroll
-    for (int b = 0; b < NB; ++b)
-        if (lane + 64 * b < nr) wh[lane + 64 * b] = acc[b];
     __syncthreads();
     const float hs = k.geo.hscale[p];
+    const double* whs = reinterpret_cast<const double*>(smem + L.hist);
     for (int t = threadIdx.x; t < nr; t += blockDim.x) {
-        float s = 0.f;
-        for (int w = 0; w < kWaves; ++w) s += smem[L.hist + w * nr + t];
+        double sd = 0.0;
+        for (int w = 0; w < kWaves; ++w) sd += whs[w * nr + t];
+        const float s = (float)sd;
         if (nsp > 1)
             k.hpart[((size_t)gsplit * k.geo.nwall + p) * nr + t] = s;
         else
@@ -2462,7 +2606,13 @@ int bwd_nsplit_ws(const nlosgr_gaussians* g, const nlosgr_geometry* geo0, const 
 
 template <int PRESET, int MODE, bool DENSE, bool RAYS, bool CACHE>
 void launch_fwd(const KArgs& ka, size_t shm, hipStream_t s) {
-    const dim3 grid(ka.geo.nwall, ka.hpart ? ka.nfsplit : 1);
+    const dim3 grid(ka.geo.nwall, (ka.hpart || ka.hfx) ? ka.nfsplit : 1);
+    if constexpr (MODE == NLOSGR_MODE_NOOCL && !DENSE && !RAYS && !CACHE) {
+        if (ka.hfx) {   // run_fwd decided the fixed-point TAIL drain (fx_eligible)
+            hipLaunchKernelGGL((fwd_kernel<PRESET, MODE, DENSE, RAYS, CACHE, true, true>), grid, dim3(kBlock), shm, s, ka);
+            return;
+        }
+    }
     constexpr bool kCanTail = (MODE == NLOSGR_MODE_NOOCL || MODE == NLOSGR_MODE_NETF || MODE == NLOSGR_MODE_BININT) &&
                               !DENSE && !RAYS;
     // NLOSGR_FTAIL=0: masked forward drain at every cutoff (A/B and parity cross-check); netf takes the
@@ -2545,9 +2695,22 @@ int fwd_nsplit(const nlosgr_gaussians* g, const nlosgr_geometry* geo) {
     if (ns > 8) ns = 8;
     return ns < 1 ? 1 : ns;
 }
+// forward partials: float [nfsplit][P][nr] (float drains) or, for the FX drain, u64 [P][nr] + the
+// amplitude-bound word at the end
 size_t fpart_bytes(const nlosgr_gaussians* g, const nlosgr_geometry* geo) {
     const int ns = fwd_nsplit(g, geo);
-    return ns > 1 ? align_up((size_t)ns * geo->nwall * geo->nr * sizeof(float)) : 0;
+    const size_t fl = ns > 1 ? (size_t)ns * geo->nwall * geo->nr * sizeof(float) : 0;
+    const size_t fx = (size_t)geo->nwall * geo->nr * sizeof(unsigned long long);
+    return align_up(fl > fx ? fl : fx) + 256;
+}
+// the fixed-point TAIL drain serves the culled no-occlusion histogram at cutoff >= kTailCutoff
+// (NLOSGR_FFX=0: the float claim drain instead, A/B)
+bool fx_eligible(const nlosgr_options* opt, bool dense, bool rays, bool counts, bool hist, bool cache) {
+    const char* e = getenv("NLOSGR_FFX");
+    const char* ft = getenv("NLOSGR_FTAIL");
+    const char* fsw = getenv("NLOSGR_FSWEEP");
+    return opt->mode == NLOSGR_MODE_NOOCL && opt->cutoff >= kTailCutoff && !dense && !rays && !counts && hist && !cache &&
+           !(e && e[0] == '0') && !(ft && ft[0] == '0') && !(fsw && fsw[0] == '1');
 }
 // after the ray cache: drho [P][ng] | sh partials [nsh][ng][kShPart] | 256-B diagnostics tail |
 // forward split partial histograms [nfsplit][P][nr]
@@ -2576,10 +2739,28 @@ int run_fwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_
     ka.counts = counts;
     if (!counts) cache_ptrs(g, geo, opt, workspace, bwd_nsplit_ws(g, geo, opt), ka);
     const int nfs = fwd_nsplit(g, geo);
-    if (hist_out && nfs > 1 && g->ng > 0) {
-        ka.hpart = (float*)((char*)workspace + align_up((size_t)g->ng * sizeof(GaussRec)) +
-                            align_up((size_t)bwd_nsplit_ws(g, geo, opt) * g->ng * 32 * sizeof(float)) +
-                            cache_bytes(g, geo, opt) + sh_bytes(g, geo) + 256);
+    const bool dense = !(opt->cutoff > 0.f);
+    const bool rays = ray_out != nullptr;
+    char* fpart = g->ng > 0 ? (char*)workspace + align_up((size_t)g->ng * sizeof(GaussRec)) +
+                                  align_up((size_t)bwd_nsplit_ws(g, geo, opt) * g->ng * 32 * sizeof(float)) +
+                                  cache_bytes(g, geo, opt) + sh_bytes(g, geo) + 256
+                            : nullptr;
+    const bool fx = g->ng > 0 && fx_eligible(opt, dense, rays, counts != nullptr, hist_out != nullptr, ka.cmask != nullptr);
+    if (fx) {
+        ka.hfx = (unsigned long long*)fpart;
+        unsigned* amax = (unsigned*)(fpart + fpart_bytes(g, geo) - 256);
+        ka.fx_amax = amax;
+        ka.nfsplit = nfs;
+        HIPCHK(hipMemsetAsync(ka.hfx, 0, (size_t)geo->nwall * geo->nr * sizeof(unsigned long long), s));
+        HIPCHK(hipMemsetAsync(amax, 0, sizeof(unsigned), s));
+        const int nb = (g->ng + kBlock - 1) / kBlock;
+        if (g->preset == NLOSGR_PRESET_TORCH)
+            hipLaunchKernelGGL(fx_amax_kernel<NLOSGR_PRESET_TORCH>, dim3(nb), dim3(kBlock), 0, s, *g, amax);
+        else
+            hipLaunchKernelGGL(fx_amax_kernel<NLOSGR_PRESET_CUDA>, dim3(nb), dim3(kBlock), 0, s, *g, amax);
+        HIPCHK(hipGetLastError());
+    } else if (hist_out && nfs > 1 && g->ng > 0) {
+        ka.hpart = (float*)fpart;
         ka.nfsplit = nfs;
     }
     if (g->ng > 0) {
@@ -2587,8 +2768,6 @@ int run_fwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_
         HIPCHK(hipGetLastError());
     }
     const size_t shm = (size_t)FwdLayout(geo->nr, geo->nt, geo->np).total * sizeof(float);
-    const bool dense = !(opt->cutoff > 0.f);
-    const bool rays = ray_out != nullptr;
     // NLOSGR_FDREG=0 routes the dense histogram through fwd_kernel instead (parity cross-check in tests)
     const char* fdreg = getenv("NLOSGR_FDREG");
     if (dense && !rays && !counts && hist_out && opt->mode == NLOSGR_MODE_NOOCL && geo->nr <= 1024 &&
@@ -2632,7 +2811,12 @@ int run_fwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_
         else dispatch_fwd<1, 2>(ka, dense, rays, shm, s);
     }
     HIPCHK(hipGetLastError());
-    if (ka.hpart) {
+    if (ka.hfx) {
+        const long long n = (long long)geo->nwall * geo->nr;
+        hipLaunchKernelGGL(fx_reduce_kernel, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, ka.hfx,
+                           ka.fx_amax, (long long)geo->nwall, geo->nr, geo->att, geo->hscale, hist_out);
+        HIPCHK(hipGetLastError());
+    } else if (ka.hpart) {
         const long long n = (long long)geo->nwall * geo->nr;
         hipLaunchKernelGGL(hist_reduce_kernel, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, ka.hpart,
                            ka.nfsplit, (long long)geo->nwall, geo->nr, geo->att, geo->hscale, hist_out);

@@ -110,7 +110,18 @@ def allreduce_step(grads, loss4, n_total, group=None, async_op=False):
     return finish()
 
 
-def slab_order(mu, wall, slabs=8, cells=4, size=None, size_buckets=0):
+def wall_centroid(wall, group=None):
+    """Centroid of the WHOLE relay wall.  With a wall shard per rank (world > 1) the sum and count of
+    every rank's wall points are all-reduced, so every rank gets the same centroid (slab_order's axis
+    must not depend on which band a rank renders)."""
+    w = wall.detach().reshape(-1, 3).double()
+    s = torch.cat([w.sum(0), torch.tensor([float(w.shape[0])], dtype=torch.float64, device=w.device)])
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+        dist.all_reduce(s, op=dist.ReduceOp.SUM, group=group)
+    return (s[:3] / s[3].clamp_min(1.0)).float()
+
+
+def slab_order(mu, wall, slabs=8, cells=4, size=None, size_buckets=0, centroid=None):
     """Permutation of the Gaussians for the backward: sorted by cell of a slabs x cells x cells grid over
     their bounding box, slab (the coordinate axis along which the Gaussians lie in front of the relay
     wall: the largest component of centroid(mu) - centroid(wall)) major, then the other two axes in
@@ -120,10 +131,12 @@ def slab_order(mu, wall, slabs=8, cells=4, size=None, size_buckets=0):
     together instead of waiting for its largest pair.  C3 backward (same box, scripts/env_ab.sh):
     given order 951 ms, 16x8 cells 937, 8x4 cells + size 887; size-quantile-major buckets 911
     (`size_buckets`).  Any order gives the same gradients up to fp32 summation order.
-    Rank-consistent: the ranks of a wall shard hold the same Gaussians and their bands' centroids
-    pick the same axis, so their permutations agree (the bucketed all-reduce sums rows in this order)."""
+    Rank-consistent: `centroid` (wall_centroid: the whole wall's, all-reduced) replaces the centroid of
+    `wall`, so the ranks of a wall shard, which hold the same Gaussians, compute the same permutation
+    whatever their bands (the bucketed all-reduce sums gradient rows in this order)."""
     with torch.no_grad():
-        d = mu.mean(0) - wall.reshape(-1, 3).mean(0)
+        wc = centroid.to(mu.device, mu.dtype) if centroid is not None else wall.reshape(-1, 3).mean(0)
+        d = mu.mean(0) - wc
         k = int(torch.argmax(d.abs()))
         axes = [k] + [i for i in range(3) if i != k]
         q = mu[:, axes]
@@ -231,8 +244,9 @@ class TrainStep:
         # NLOSGR_FWD_ORDER=0 disable them (A/B)
         self.bwd_order = None if os.environ.get("NLOSGR_BWD_ORDER") == "0" else bwd_order
         self.fwd_order = None if os.environ.get("NLOSGR_FWD_ORDER") == "0" else fwd_order
-        self.keep_grads = keep_grads   # tests: keep the last step's (all-reduced) gradients in self.grads
-        self.grads = None
+        self.keep_grads = keep_grads   # tests: keep the last step's (all-reduced) gradients in self.grads,
+        self.grads = None              # its forward volume in self.hist and its dL/dhist in self.grad_hist
+        self.hist = self.grad_hist = None
         self.target = target.detach().float().contiguous()
         self.gt_times = float(gt_times)
         self.opt = opt or OptimizationParams()
@@ -251,6 +265,8 @@ class TrainStep:
         self.buckets = int(buckets)   # gradient all-reduce buckets overlapped with the backward (world > 1)
         self.iteration = 0
         self._batch_events = []
+        # the slab orders' axis comes from the whole wall's centroid (the same on every rank)
+        self.wall_c = wall_centroid(geo.wall, group) if self.world > 1 else wall_centroid(geo.wall)
         ng = model._mu.shape[0]
         self._tensors = [model._mu.data, model._features_dc.data.view(ng, -1), model._features_rest.data.view(ng, -1),
                          model._opacity.data.view(ng), model._scaling.data, model._rotation.data]
@@ -369,7 +385,7 @@ class TrainStep:
             # slabs keep them spread over the ToF bins (claim collisions).  C3 forward 1086 -> 1050 ms;
             # 4 / 16 / 32 slabs the same, no slabs (size only) 1077, with lateral cells 1101.  The
             # histogram is order-independent up to fp32 summation order.
-            fp = slab_order(args[0], self.geo.wall, 8, 1, size=args[1].max(1).values)
+            fp = slab_order(args[0], None, 8, 1, size=args[1].max(1).values, centroid=self.wall_c)
             out = render_forward(*(tuple(t[fp].contiguous() for t in args[:5]) + (args[5],)), cfg, True, False,
                                  ray_cache=cache)
         else:
@@ -379,6 +395,8 @@ class TrainStep:
         hist, ws = out[0], (out[2] if cache else None)
         loss4, grad = mse(hist, self.target, self.gt_times, grad_scale=self.n_local / self.n_total, raw=True)
         loss2 = loss4[:2]
+        if self.keep_grads:
+            self.hist, self.grad_hist = hist, grad
         if ev:
             ev["bwd"][0].record(stream)
         bounds = bucket_bounds(ng, self.buckets) if (self.world > 1 and cfg.mode != "occl"
@@ -391,8 +409,8 @@ class TrainStep:
             sc = tuple(int(v) for v in sl.split(",")) if sl else (8, 4)   # 1 = max log-scale, 2 = log-volume
             sz = os.environ.get("NLOSGR_SLAB_SIZE", "1")
             size = args[1].max(1).values if sz == "1" else (args[1].sum(1) if sz == "2" else None)
-            perm = slab_order(args[0], self.geo.wall, *sc, size=size,
-                              size_buckets=int(os.environ.get("NLOSGR_SLAB_SIZEB", "0")))
+            perm = slab_order(args[0], None, *sc, size=size,
+                              size_buckets=int(os.environ.get("NLOSGR_SLAB_SIZEB", "0")), centroid=self.wall_c)
             args = tuple(t[perm].contiguous() for t in args[:5]) + (args[5],)
 
         def unperm(gs):

@@ -1,0 +1,93 @@
+// Microbenchmark (diagnostic, not product): the forward drain's scatter-add into a wave's LDS
+// histogram, float2 read-add-write (the claim drain's access) against packed fixed-point
+// ds_add_u64 (two 32-bit bin fields per 64-bit word, no claims), at random and at clustered start
+// bins (the real drain's segments of one wave start near each other).  Reported per BIN.
+//   mode 0: float2 read-add-write, random even starts          (2 bins per op pair)
+//   mode 1: ds_add_u64 packed, random even starts              (2 bins per op)
+//   mode 2: float2 read-add-write, starts within 48 bins of a wave base
+//   mode 3: ds_add_u64 packed, starts within 48 bins of a wave base
+//   mode 4: ds_add_u64 packed, starts within 12 bins of a wave base (heavy clustering)
+//   mode 5: float2 read-add-write, starts within 12 bins of a wave base
+//   mode 6: ds_add_u64 packed, distinct consecutive pairs (lane l at base + 2l: conflict-free)
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdint.h>
+
+__device__ __forceinline__ unsigned cvt_rpi(float x) {   // floor(x + 0.5) as an integer, one VALU op
+    int r;
+    __asm__("v_cvt_rpi_i32_f32 %0, %1" : "=v"(r) : "v"(x));
+    return (unsigned)r;
+}
+
+constexpr int kBins = 1024, kSteps = 20, kIters = 2000, kBlocks = 256 * 12;
+
+template <int MODE>
+__global__ __launch_bounds__(256) void bench(float* out, int seed) {
+    constexpr bool ATOM = MODE == 1 || MODE == 3 || MODE == 4 || MODE == 6;
+    constexpr int SPREAD = (MODE == 2 || MODE == 3) ? 48 : ((MODE == 4 || MODE == 5) ? 12 : 0);
+    __shared__ __align__(16) unsigned h32[4 * (kBins + 192)];
+    for (int t = threadIdx.x; t < 4 * (kBins + 192); t += 256) h32[t] = 0u;
+    __syncthreads();
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    unsigned st = (unsigned)(lane * 2654435761u) ^ (unsigned)(seed + blockIdx.x * 7919);
+    float v = 1.0f + lane * 1e-3f;
+    const int wbase = wave * (kBins + 192);
+    for (int it = 0; it < kIters; ++it) {
+        st = st * 1664525u + 1013904223u;
+        int pos;
+        if (MODE == 6) {
+            pos = (int)(__builtin_amdgcn_readfirstlane((st >> 8) % (kBins - 160)) & ~1) + 2 * lane;
+        } else if (SPREAD) {
+            const unsigned b = __builtin_amdgcn_readfirstlane((st >> 8) % (kBins - kSteps - SPREAD));
+            pos = (int)(b + ((st >> 20) % SPREAD)) & ~1;
+        } else {
+            pos = (int)((st >> 8) % (kBins - kSteps)) & ~1;
+        }
+        if (!ATOM) {
+            float2* hb = reinterpret_cast<float2*>(reinterpret_cast<float*>(h32) + wbase + pos);
+#pragma unroll
+            for (int m = 0; m < kSteps / 2; ++m) {
+                float2 x = hb[m];
+                x.x += v; x.y += v * 0.5f;
+                hb[m] = x;
+                __asm__ __volatile__("" ::: "memory");
+            }
+        } else {
+            unsigned long long* hb = reinterpret_cast<unsigned long long*>(h32 + wbase + pos);
+#pragma unroll
+            for (int m = 0; m < kSteps / 2; ++m) {
+                const unsigned lo = (unsigned)cvt_rpi((float)m * v), hi = (unsigned)cvt_rpi(v);
+                __hip_atomic_fetch_add(hb + m, ((unsigned long long)hi << 32) | lo, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+        }
+        v = v * 1.0001f;
+    }
+    __syncthreads();
+    float s = 0.f;
+    for (int t = threadIdx.x; t < 4 * (kBins + 192); t += 256) s += (float)(h32[t] & 0xffff);
+    out[blockIdx.x * 256 + threadIdx.x] = s;
+}
+
+template <int MODE>
+void run(float* d) {
+    hipEvent_t a, b;
+    hipEventCreate(&a); hipEventCreate(&b);
+    bench<MODE><<<kBlocks, 256>>>(d, 1);
+    hipEventRecord(a);
+    bench<MODE><<<kBlocks, 256>>>(d, 2);
+    hipEventRecord(b);
+    hipEventSynchronize(b);
+    float ms; hipEventElapsedTime(&ms, a, b);
+    const double bins = (double)kBlocks * 4 * kIters * kSteps;   // wave bin-steps
+    printf("mode %d: %.3f ms  %.2f CU-cycles per wave bin-step (2.4 GHz, 256 CUs)\n", MODE, ms,
+           ms * 1e-3 * 2.4e9 * 256 / bins);
+}
+
+int main() {
+    float* d;
+    hipMalloc(&d, kBlocks * 256 * sizeof(float));
+    run<0>(d); run<1>(d); run<2>(d); run<3>(d); run<4>(d); run<5>(d); run<6>(d);
+    hipFree(d);
+    return 0;
+}

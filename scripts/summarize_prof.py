@@ -74,10 +74,15 @@ def main(src, tag):
                    **wl, "kernels": res}, f, indent=1)
     # the bench line read the previously committed traffic/VALU profiles when it ran: restate its
     # roofline.traffic from the passes of this same run
-    kl = line["roofline"]["kernel"].split("(", 1)[1].rstrip(")").split(" + ")
-    hits = [[v["hbm_bytes_per_step"] for k, v in res.items() if sub in k] for sub in kl]
-    if all(hits):
-        line["roofline"]["traffic"] = sum(max(h) for h in hits)
+    sys.path.insert(0, ROOT)
+    from bench import phase_traffic
+    tiles = wl["mode"] == "occl" or wl["selection"] == "aabb"
+    dom = line["roofline"]["kernel"].split()[1]          # "nlosgr fwd (...)" / "nlosgr bwd (...)"
+    per = {ph: phase_traffic(res, ("tiles_" + ph) if tiles else ph)[0] for ph in ("fwd", "bwd")}
+    if per.get(dom) is not None:
+        line["roofline"]["traffic"] = per[dom]
+        line["roofline"]["traffic_per_phase"] = {"fwd": per["fwd"], "bwd": per["bwd"],
+                                                 "unit": "HBM bytes per step (PMC FETCH_SIZE x2 + WRITE_SIZE)"}
         line["roofline"]["traffic_source"] = f"profiles/{tag}_traffic.json"
     sqf = glob.glob(os.path.join(src, "sq_*counter_collection.csv"))
     if sqf:

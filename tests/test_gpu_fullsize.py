@@ -149,9 +149,10 @@ def test_c2_full_size():
 
 def test_c3_full_size_train_step_parity():
     """C3 (the headline): 100k Gaussians -> 128x128 wall x 1024 bins, cuda preset, cutoff 5.7 sigma,
-    forward + backward exactly as TrainStep runs them (the ray cache per use_ray_cache).  Whole volume finite;
-    2 wall points vs the dense HIP evaluation (hist and gradients seeded there); a Gaussian subset vs
-    the oracle."""
+    the forward and backward kernels TrainStep runs (ray cache per use_ray_cache), called directly in
+    the given Gaussian order (TrainStep's own slab orders: test_c3_trainstep_full_ng_accuracy).  Whole
+    volume finite; 2 wall points vs the dense HIP evaluation (hist and gradients seeded there); a
+    Gaussian subset vs the oracle."""
     from nlosgr import GaussianParams
     from nlosgr.render import render_backward, render_forward, use_ray_cache
     from nlosgr.volume import Scene, make_config
@@ -185,6 +186,62 @@ def test_c3_full_size_train_step_parity():
     for name, a, b in zip(("mu", "scaling", "rotation", "opacity", "dc", "rest"), _hip_grads_as_ref(ds), rgrads):
         assert float(b.abs().max()) > 0 or name == "rest", name
         _close(a, b, 2e-4, atol=1e-9, msg=f"C3 subset grad {name}")
+
+
+def test_c3_trainstep_full_ng_accuracy(monkeypatch):
+    """The headline's accuracy at full Ng through the exact path bench.py times: one C3 TrainStep
+    (default slab-ordered forward and backward, 5.7 sigma) with keep_grads.
+      * forward rows of 2 wall points vs the float64 sum of 400 HIP sub-histograms of 250 Gaussians each
+        (float claim drain, NLOSGR_FFX=0: a few hundred terms per bin per sub-histogram), same geometry
+        and cutoff: max error <= 2e-5 of the rows' max (gaussian_model.py:346-364, nlos_helpers.py:228-229
+        sum over all Gaussians);
+      * all six gradients vs the unordered render_backward seeded with the step's own dL/dhist, on the
+        step's input parameters: fp32 summation order only, within the suite's gradient tolerance (2e-4
+        of each tensor's max; measured 1.2e-7 - 1.8e-7, rotation 3.6e-5: its chain through the
+        quaternion Jacobian cancels, which magnifies the order noise of dL/dA)."""
+    from nlosgr import GaussianParams
+    from nlosgr.render import render_backward, render_forward
+    from nlosgr.train import TrainStep
+    from nlosgr.volume import Scene, make_config
+    dev = torch.device("cuda:0")
+    ng, T = 100_000, 1024
+    scene = Scene(H=128, W=128, T=T, ns=32)
+    m = GaussianParams.synthetic(ng, 3, preset="cuda", device=dev, seed=0)
+    geo = scene.geometry(dev, "cuda", "noocl")
+    cfg = make_config(m, scene, "cuda", "noocl", cutoff=PARITY_CUTOFF)
+    gt = torch.Generator().manual_seed(1)
+    target = (torch.rand(128 * 128, T, generator=gt) * 1e-3).to(dev)
+    before = [t.detach().clone() for t in (m._mu, m._scaling, m._rotation, m._opacity, m._features_dc,
+                                           m._features_rest)]
+    step = TrainStep(m, geo, cfg, target, gt_times=100.0, keep_grads=True)
+    assert step.fwd_order == "slab" and step.bwd_order == "slab"
+    step()
+    torch.cuda.synchronize()
+    hist, gh, grads = step.hist, step.grad_hist, step.grads
+    with torch.no_grad():      # back to the step's inputs (Adam moved them)
+        for t, b in zip((m._mu, m._scaling, m._rotation, m._opacity, m._features_dc, m._features_rest), before):
+            t.copy_(b)
+    idx = torch.tensor([128 * 40 + 30, 128 * 100 + 90], device=dev)
+    gsel = scene.geometry(dev, "cuda", "noocl", walls=geo.wall[idx].contiguous())
+    monkeypatch.setenv("NLOSGR_FFX", "0")
+    ref = torch.zeros(len(idx), T, dtype=torch.float64, device=dev)
+    for g0 in range(0, ng, 250):
+        sub = _subset(m, torch.arange(g0, min(ng, g0 + 250), device=dev))
+        h, _ = render_forward(*_params(sub), gsel, make_config(sub, scene, "cuda", "noocl", cutoff=PARITY_CUTOFF))
+        ref += h.double()
+    monkeypatch.delenv("NLOSGR_FFX")
+    a = hist[idx].double()
+    err = float((a - ref).abs().max() / ref.abs().max())
+    rel2 = float((a - ref).norm() / ref.norm())
+    print(f"C3 TrainStep forward vs float64 sub-histogram sum: max err {err:.3e} of max, rel-L2 {rel2:.3e}")
+    assert err <= 2e-5, err
+    d_mu, d_s, d_q, d_o, d_f = render_backward(*_params(m), geo, cfg, grad_hist=gh)
+    ref_g = [d_mu, d_f[:, :1], d_f[:, 1:], d_o, d_s, d_q]
+    for name, a, b in zip(("mu", "f_dc", "f_rest", "opacity", "scaling", "rotation"), grads, ref_g):
+        a, b = a.reshape(b.shape).double(), b.double()
+        e = float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
+        print(f"C3 TrainStep ordered backward vs unordered: {name} max err {e:.3e} of max")
+        assert e <= 2e-4, (name, e)
 
 
 def test_c4_full_size_binint_vs_numerical():
