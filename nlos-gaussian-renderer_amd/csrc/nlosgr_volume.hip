@@ -13,14 +13,15 @@
 //               (exactly m2min <= m_c^2), then
 //   * per ray:  one contiguous bin range [kl, kh] (a "segment").
 //
-// Work decomposition (4 independent waves per workgroup; no global atomics on the hot path):
-//   forward : workgroup = one wall point.  Lane = (wall point, Gaussian) pair enumerates its
-//             candidate rays; passing rays become segments in a wave-private LDS queue.  The
-//             queue is drained 64 bins at a time with lane = bin: conflict-free adds into a
-//             wave-private LDS histogram, flushed periodically (round-to-nearest) into a
-//             wave-private total (LDS float atomics accumulate with a downward bias when a bin
-//             collects thousands of adds).  The 4 totals are summed in a fixed order, so the
-//             forward is bitwise deterministic.
+// Work decomposition (4 independent waves per workgroup):
+//   forward : workgroup = one wall point x a split of the Gaussians.  Lane = (wall point,
+//             Gaussian) pair enumerates its candidate rays; passing rays become segments in a
+//             wave-private LDS queue.  Lane = segment then walks its bins with the exp2 recurrence
+//             and adds them into a wave-private LDS histogram: at the training cutoff as fixed-point
+//             integers, two bins per no-return ds_add_u64 (FX drain: no claims, order-independent,
+//             exact up to one rounding per term), otherwise as float2 read-add-writes with a claim
+//             table keeping the lanes' addresses distinct.  Either way the forward is bitwise
+//             deterministic (FX: integer sums; float: fixed-order wave and split reductions).
 //   backward: workgroup = 64 Gaussians x a split of the wall; wave w walks wall points
 //             w, w+4, ...  Lane = segment runs the bins of one ray serially with its sums in
 //             registers; per-pair sums in LDS; per-Gaussian accumulators stay in registers
@@ -281,11 +282,13 @@ constexpr int kBRefill = NLOSGR_BREFILL;   // backward: same rule
 
 struct FwdLayout {
     int hist, owner, rayq, wave_stride, total;  // offsets in floats
-    __host__ __device__ FwdLayout(int nr, int nt, int np_) {
+    // fx: the fixed-point drain needs no claim table and no per-lane pad bins (22.7 KB per C3
+    // workgroup instead of 26.6 KB: 7 workgroups per CU)
+    __host__ __device__ FwdLayout(int nr, int nt, int np_, bool fx = false) {
         const int off = al4(2 * (nt + np_));  // float2 theta table [nt], float2 phi table [np]
-        hist = 0;                             // [nr + kSteps] bins + [kSteps + 64] pad bins
-        owner = al4(nr + 2 * kSteps + 64);    // u8 [nr] claim table
-        rayq = owner + al4((nr + 3) / 4);     // uint [kRQ] ring
+        hist = 0;                             // [nr + kSteps] bins + [kSteps + 64] pad bins (fx: [nr + kSteps + 2])
+        owner = fx ? al4(nr + kSteps + 4) : al4(nr + 2 * kSteps + 64);   // u8 [nr] claim table
+        rayq = owner + (fx ? 0 : al4((nr + 3) / 4));   // uint [kRQ] ring
         wave_stride = al4(rayq + kRQ);
         hist += off; owner += off; rayq += off;
         total = off + kWaves * wave_stride;
@@ -444,35 +447,12 @@ __device__ __forceinline__ void compiler_fence() { __asm__ __volatile__("" ::: "
 // Gaussian's peak (<= 3.7e-6 at m_c >= kTailCutoff), so the result lies between the culled and the
 // dense sum.  Bins past nr land in the zeroed pad row.
 constexpr float kTailCutoff = 5.0f;
-// Conveyor drain (TAIL no-occlusion float2 drain): lane l only ever holds a segment whose current bin
-// pair is = l + (kSteps / 2) R (mod 64) in drain round R.  Every active lane advances kSteps / 2 pairs per
-// round, so the invariant holds round after round, the 64 lanes always write 64 distinct pairs (no claim
-// table) and each 16-lane group of a ds_write_b64 (32-lane half of a ds_read_b64) covers 16 (32)
-// consecutive pairs: no bank conflicts.  A new segment is placed, at refill, in the free lane at or
-// below its residue's lane; a lane d below its own starts d pairs before its support (the Gaussian's
-// exact values there, as past its end; only while the seed stays >= 2^-120).  Placement: up to
-// kPlaceIters rounds of forward-permute claims on free lanes, then the winners' drain state moves by
-// bpermute; segments left unplaced go back to the head of the ray queue.  0 = claim-table drain.
-#ifndef NLOSGR_FCONV
-#define NLOSGR_FCONV 0
-#endif
-constexpr bool kFConv = NLOSGR_FCONV != 0;
-#ifndef NLOSGR_PLACE_ITERS
-#define NLOSGR_PLACE_ITERS 3
-#endif
-constexpr int kPlaceIters = NLOSGR_PLACE_ITERS;
-#ifndef NLOSGR_PLACE_SPREAD
-#define NLOSGR_PLACE_SPREAD 8
-#endif
-constexpr int kPlaceSpread = NLOSGR_PLACE_SPREAD;   // power of two
 // debug build (-DNLOSGR_FCOUNT, scripts/drain_counts.py): count_support runs the TAIL forward and returns
 // (wave drain rounds, active lanes summed over rounds, claim winners summed) instead of its work counts
 #ifdef NLOSGR_FCOUNT
 #define NLOSGR_FCOUNT_ON 1
-#define NLOSGR_FCOUNT_MODE (NLOSGR_FCOUNT + 0)   // 2: conveyor placement (refills, leftovers, shift pairs)
 #else
 #define NLOSGR_FCOUNT_ON 0
-#define NLOSGR_FCOUNT_MODE 0
 #endif
 constexpr float kBetaSeries = 0.5f;   // bin-integrated TAIL drain: series bin average up to this beta
 
@@ -511,11 +491,11 @@ template <int PRESET, int MODE, bool DENSE, bool RAYS, bool CACHE, bool TAIL = f
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) void fwd_kernel(KArgs k) {
     extern __shared__ __align__(16) float smem[];
     const int nr = k.geo.nr, nt = k.geo.nt, np_ = k.geo.np;
-    const FwdLayout L(nr, nt, np_);
+    const FwdLayout L(nr, nt, np_, FX);
     static_assert(!FX || (TAIL && MODE == NLOSGR_MODE_NOOCL && !DENSE && !RAYS), "fixed-point drain: TAIL no-occlusion histogram");
     float2* tth = reinterpret_cast<float2*>(smem);
     float2* tph = tth + nt;
-    const int wave = threadIdx.x >> 6, lane = lane_id();
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = lane_id();   // wave-uniform (SGPR)
     float* wb = smem + wave * L.wave_stride;
     float* hist = wb + L.hist;
     unsigned char* owner = reinterpret_cast<unsigned char*>(wb + L.owner);
@@ -531,7 +511,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
         tth[t] = make_float2(k.geo.sin_theta[(size_t)p * nt + t], k.geo.cos_theta[(size_t)p * nt + t]);
     for (int t = threadIdx.x; t < np_; t += blockDim.x)
         tph[t] = make_float2(k.geo.cos_phi[(size_t)p * np_ + t], k.geo.sin_phi[(size_t)p * np_ + t]);
-    for (int t = lane; t < nr + 2 * kSteps + 64; t += 64) hist[t] = 0.f;
+    for (int t = lane; t < (FX ? nr + kSteps + 4 : nr + 2 * kSteps + 64); t += 64) hist[t] = 0.f;
     __syncthreads();
 
     const float px = k.geo.wall[3 * p], py = k.geo.wall[3 * p + 1], pz = k.geo.wall[3 * p + 2];
@@ -566,7 +546,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
     d.wrap = 0; d.tw = 0.f;
     bool act = false;
     int qhead = 0, qcount = 0;
-    unsigned conv_r = 0;   // conveyor: drain rounds so far (wave-uniform)
 
     for (int base = g_lo + wave * 64;; base += kBlock) {
         const bool have = base < g_hi;         // wave-uniform
@@ -638,81 +617,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
                 const int ntake = min(nidle, qcount);
                 qhead = (qhead + ntake) & (kRQ - 1);
                 qcount -= ntake;
-                if (kFConv && QUADF && TAIL && MODE == NLOSGR_MODE_NOOCL) {
-                    // place this refill's segments (lanes `take && act`) on free lanes of their residue
-                    const bool newl = take && act;
-                    unsigned long long avail = __builtin_amdgcn_ballot_w64(!act || take);   // no old segment
-                    const int k0 = d.pos >> 1, o = d.pos & 1;
-                    const int r0 = (k0 - (int)(conv_r * (unsigned)(kSteps / 2))) & 63;
-                    // pairs the start may move down: the seed at bin 2 (k0 - s) keeps d.ga t^2 + d.al >= -120
-                    const float span = d.al + 120.f;
-                    const float tm = span > 0.f ? sqrtf(span / fmaxf(-d.ga, 1e-30f)) : 0.f;
-                    const int smax = newl ? min(k0, (int)floorf(0.5f * (d.t - (float)o + tm))) : 0;
-                    bool unpl = newl, placed = false;
-                    int src = lane, dsh = 0;
-                    bool recv_any = false;
-#pragma unroll
-                    for (int itp = 0; itp < kPlaceIters; ++itp) {
-                        const unsigned long long um = __builtin_amdgcn_ballot_w64(unpl);
-                        if (!um) break;
-                        // segments of one pair start on the same residue: spread the senders over the
-                        // kPlaceSpread lanes below it by their rank, then take the nearest free lane below
-                        const int j0 = (lanes_below(um) + 3 * itp) & (kPlaceSpread - 1);
-                        const int rs = (r0 - j0) & 63;
-                        const int sr = 63 - rs;   // rotate: bit 63 <-> lane rs, bit 63 - s <-> lane rs - s
-                        const unsigned long long x = sr ? ((avail << sr) | (avail >> (64 - sr))) : avail;
-                        const int dl = x ? (int)__builtin_clzll(x) + j0 : 64;
-                        const bool can = unpl && dl <= max(smax, 0) && dl < 64;
-                        const int tg = (r0 - dl) & 63;
-                        // forward-permute claim (highest sender wins a lane; see the backward hand-off)
-                        const int pv = can ? lane + 1 : 0;
-                        const int w1 = __builtin_amdgcn_ds_permute((can ? tg : 0) << 2, pv);
-                        const int w2 = __builtin_amdgcn_ds_permute((can ? tg : 1) << 2, pv);
-                        const int wcl = lane == 0 ? w2 : w1;
-                        const int back = __builtin_amdgcn_ds_bpermute(tg << 2, wcl);
-                        const bool won = can && back == lane + 1;
-                        if (wcl != 0) { src = wcl - 1; recv_any = true; }
-                        if (won) { placed = true; dsh = dl; }
-                        if (won || !can) unpl = false;   // !can: nothing free within reach -> back to the queue
-                        avail &= ~__builtin_amdgcn_ballot_w64(wcl != 0);
-                    }
-                    const bool leftover = newl && !placed;
-                    if (NLOSGR_FCOUNT_MODE == 2) {
-                        npair += 1u;
-                        nseg += (unsigned)__popcll(__builtin_amdgcn_ballot_w64(leftover));
-                        nsamp += placed ? (unsigned)dsh : 0u;
-                    }
-                    // placed segments start dsh pairs lower (dsh > 0: at the even bin, seeded there)
-                    int npos = d.pos, nrem = d.rem;
-                    float nt_ = d.t;
-                    if (placed && dsh > 0) {
-                        npos = 2 * (k0 - dsh);
-                        nrem = d.rem + o + 2 * dsh;
-                        nt_ = d.t - (float)(o + 2 * dsh);
-                    }
-                    // move: every lane reads its source lane's state (its own when it received nothing)
-                    const int sa = src << 2;
-                    const int mpos = __builtin_amdgcn_ds_bpermute(sa, npos);
-                    const int mrem = __builtin_amdgcn_ds_bpermute(sa, nrem);
-                    const float mt = __int_as_float(__builtin_amdgcn_ds_bpermute(sa, __float_as_int(nt_)));
-                    const float mga = __int_as_float(__builtin_amdgcn_ds_bpermute(sa, __float_as_int(d.ga)));
-                    const float mal = __int_as_float(__builtin_amdgcn_ds_bpermute(sa, __float_as_int(d.al)));
-                    if (recv_any) {
-                        d.pos = mpos; d.rem = mrem; d.t = mt; d.ga = mga; d.al = mal;
-                        act = true;
-                    } else if (newl) {
-                        act = false;   // its segment moved out, or goes back to the queue
-                    }
-                    // unplaced segments: their queue entries back to the head of the ring
-                    const unsigned long long lm = __builtin_amdgcn_ballot_w64(leftover);
-                    if (lm) {
-                        const int nl = __popcll(lm);
-                        qhead = (qhead - nl) & (kRQ - 1);
-                        if (leftover) rayq[(qhead + lanes_below(lm)) & (kRQ - 1)] = e;
-                        qcount += nl;
-                        wave_sync();
-                    }
-                }
             }
             const bool anyact = __builtin_amdgcn_ballot_w64(act) != 0;
             if (!anyact) {
@@ -723,8 +627,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
             // claim distinct start keys (distinct addresses; vector drain: distinct start pairs)
             constexpr bool QUAD = QUADF;
             constexpr int VW = 2;   // bins per LDS read-add-write of the vector drain (float2)
-            constexpr bool CONV = kFConv && QUADF && TAIL && MODE == NLOSGR_MODE_NOOCL;
-            bool win = act;   // conveyor: distinct pairs by construction; FX: integer adds, no claims
+            bool win = act;   // FX: integer adds, no claims
             if (FX && __builtin_amdgcn_ballot_w64(fxs > fthr)) {
                 // a lane passed its share of the headroom: read the fields' true maximum (and move
                 // them to the global u64 histogram once it passes 2^31)
@@ -746,14 +649,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
                 fthr = (kFxLimit - (float)mx) * (1.0f / 64.0f);
                 fxs = act ? fpk : 0.f;   // an active segment may still add up to its peak to any bin
             }
-            if (!CONV && !FX) {
+            if (!FX) {
                 const int key = QUAD ? (d.pos / VW) : d.pos;
                 if (act) owner[key] = (unsigned char)lane;
                 wave_sync();
                 win = act && owner[key] == (unsigned char)lane;
                 wave_sync();
             }
-            if (NLOSGR_FCOUNT_ON && NLOSGR_FCOUNT_MODE != 2) {
+            if (NLOSGR_FCOUNT_ON) {
                 npair += 1u;
                 nseg += (unsigned)__popcll(__builtin_amdgcn_ballot_w64(act));
                 nsamp += (unsigned)__popcll(__builtin_amdgcn_ballot_w64(win));   // every lane: / 64 on the host
@@ -1002,7 +905,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
                 }
                 act = d.rem > 0;
             }
-            if (CONV) ++conv_r;
         }
         if (CACHE && have && base + lane < g_hi) {
             // every candidate of this chunk has been tested: record the pair's passing cells
@@ -1098,457 +1000,6 @@ __global__ __launch_bounds__(kBlock) void fx_reduce_kernel(const unsigned long l
     hist[i] = (float)((double)hfx[i] * q) * att[t] * hscale[p];
 }
 
-// ------------------------------------------------------------------------------------------
-// forward, window sweep (no-occlusion histogram at cutoff >= kTailCutoff: the training hot path)
-// ------------------------------------------------------------------------------------------
-// The lane-serial drain above is bound by the LDS array: every (segment, bin) value is one LDS
-// read-add-write at a random start bin (bank conflicts, claim losers).  Here the 64 lanes of a wave
-// walk the SAME 16-bin window [W, W+16) at a time, each on its own segment: lane l holds the values
-// of bins W..W+15 of its segment in 16 registers (exp2 seed at W, then the two-multiply recurrence),
-// and one reduce-scatter across the wave (permlane32/16 swaps, then DPP row_ror:8 / row_half_mirror /
-// quad_perm adds: 35 VALU for 1024 lane-bins) leaves every quad of lanes holding one bin's sum, which
-// one lane adds into the wave's LDS histogram: 16 conflict-free read-add-writes per window instead
-// of 1024.  For the lanes to share windows, the segments are collected in an LDS batch (records
-// ga, al, ks, kl|kh) and counting-sorted by start window ("bucket" = kl / 16); the sweep walks the
-// buckets upwards and free lanes take records of the current bucket (seeded at W <= kl: the bins
-// [W, kl) get the Gaussian's exact values outside the cutoff, as the TAIL drains' overrun past kh).
-// A free lane that finds the bucket empty takes the remainder [W, kh] of a record of the two buckets
-// behind (a "late" record); its head [kl, W - 1] ends on a window boundary and is swept in a later
-// pass, so no piece ever runs past a split point.  Lanes whose seed at W would underflow (Gaussians
-// much narrower than a bin, W < kl) take an exact per-bin exp2 path for that window.  The forward's
-// summation order is fixed by the sort and the lane order: deterministic.
-constexpr int kSW = 16;                    // bins per window (value registers per lane)
-#ifndef NLOSGR_SWEEP_CAP
-#define NLOSGR_SWEEP_CAP 640
-#endif
-constexpr int kSCap = NLOSGR_SWEEP_CAP;     // segment records per wave batch (<= 65535)
-constexpr float kSeedMin = -120.f;          // log2 of the smallest seed the recurrence starts from
-#ifndef NLOSGR_SWEEP_LATE
-#define NLOSGR_SWEEP_LATE 2
-#endif
-constexpr int kSLate = NLOSGR_SWEEP_LATE;   // windows behind W a free lane takes late remainders from
-
-struct SweepLayout {
-    int hist, ring, rec, idx, hidx, cnt, bcur, bend, wave_stride, total, nb;   // offsets in floats
-    __host__ __device__ SweepLayout(int nr, int nt, int np_) {
-        const int off = al4(2 * (nt + np_));
-        nb = (nr + kSW - 1) / kSW;
-        hist = 0;                               // [nb * kSW + kSW]: windows past nr land in the pad
-        ring = al4(nb * kSW + kSW);             // u32 [kRQ] candidate ray ring
-        rec = ring + kRQ;                       // float4 [kSCap] segment records
-        idx = rec + 4 * kSCap;                  // u16 [kSCap] bucket-sorted record ids
-        hidx = idx + al4((kSCap + 1) / 2);      // u16 [kSCap] heads left by late takes (next pass)
-        cnt = hidx + al4((kSCap + 1) / 2);      // int [nb] counting-sort cursors
-        bcur = cnt + al4(nb);                   // int [nb] next unread sorted position per bucket
-        bend = bcur + al4(nb);                  // int [nb] end of the bucket
-        wave_stride = al4(bend + nb);
-        hist += off; ring += off; rec += off; idx += off; hidx += off; cnt += off; bcur += off; bend += off;
-        total = off + kWaves * wave_stride;
-    }
-};
-
-__device__ __forceinline__ int rec_kl(float4 r) { return __float_as_int(r.w) & 0xFFFF; }
-__device__ __forceinline__ int rec_kh(float4 r) { return (int)((unsigned)__float_as_int(r.w) >> 16); }
-__device__ __forceinline__ float rec_pack(int kl, int kh) { return __int_as_float(kl | (kh << 16)); }
-
-template <int CTRL>
-__device__ __forceinline__ float dppf(float v) {
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
-}
-
-// x[r] = this lane's value of bin W + r  ->  every lane returns the wave's sum for bin W + (lane >> 2)
-__device__ __forceinline__ float window_reduce(float* x) {
-    const int lane = lane_id();
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {   // lanes 32-63 of x[j] <-> lanes 0-31 of x[j+8]: bin j + 8 (lane >> 5)
-        const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x[j]), __float_as_uint(x[j + 8]), false, false);
-        x[j] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {   // odd rows of x[j] <-> even rows of x[j+4]: + 4 ((lane >> 4) & 1)
-        const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x[j]), __float_as_uint(x[j + 4]), false, false);
-        x[j] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
-    }
-    const bool b3 = (lane & 8) != 0, b2 = (lane & 4) != 0;
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {   // lane ^ 8 (row_ror:8): + 2 ((lane >> 3) & 1)
-        const float snd = b3 ? x[j] : x[j + 2], kp = b3 ? x[j + 2] : x[j];
-        x[j] = kp + dppf<0x128>(snd);
-    }
-    float s;
-    {   // lane <-> 7 - lane within 8 (row_half_mirror): + ((lane >> 2) & 1)
-        const float snd = b2 ? x[0] : x[1], kp = b2 ? x[1] : x[0];
-        s = kp + dppf<0x141>(snd);
-    }
-    s += dppf<0xB1>(s);   // quad_perm [1,0,3,2]
-    s += dppf<0x4E>(s);   // quad_perm [2,3,0,1]
-    return s;
-}
-
-// first bucket >= from with unread records, or -1 (wave-uniform)
-__device__ __forceinline__ int next_pending(const int* bcur, const int* bend, int nb, int from) {
-    for (int b0 = from; b0 < nb; b0 += 64) {
-        const int b = b0 + lane_id();
-        const unsigned long long m = __builtin_amdgcn_ballot_w64(b < nb && bcur[b] < bend[b]);
-        if (m) return b0 + (int)__builtin_ctzll(m);
-    }
-    return -1;
-}
-
-// counting sort of the records list[0..n) (nullptr: ids 0..n-1) by bucket into idx, bucket ranges
-// [bcur, bend).  LDS atomics return in lane order within an instruction: the order is deterministic.
-__device__ void sweep_sort(const float4* rec, const unsigned short* list, int n, unsigned short* idx, int* cnt,
-                           int* bcur, int* bend, int nb) {
-    const int lane = lane_id();
-    for (int b = lane; b < nb; b += 64) cnt[b] = 0;
-    wave_sync();
-    for (int i = lane; i < n; i += 64) {
-        const int id = list ? list[i] : i;
-        atomicAdd(&cnt[rec_kl(rec[id]) / kSW], 1);
-    }
-    wave_sync();
-    const int per = (nb + 63) / 64;
-    int s = 0;
-    for (int u = 0; u < per; ++u) {
-        const int b = lane * per + u;
-        if (b < nb) s += cnt[b];
-    }
-    int incl = s;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int y = __shfl_up(incl, o);
-        if (lane >= o) incl += y;
-    }
-    int run = incl - s;
-    for (int u = 0; u < per; ++u) {
-        const int b = lane * per + u;
-        if (b < nb) {
-            const int c = cnt[b];
-            bcur[b] = run;
-            bend[b] = run + c;
-            cnt[b] = run;
-            run += c;
-        }
-    }
-    wave_sync();
-    for (int i = lane; i < n; i += 64) {
-        const int id = list ? list[i] : i;
-        const int pos = atomicAdd(&cnt[rec_kl(rec[id]) / kSW], 1);
-        idx[pos] = (unsigned short)id;
-    }
-    wave_sync();
-}
-
-// sweep the batch rec[0..n) into the wave's histogram (see above); leaves the batch empty
-#ifdef NLOSGR_SWEEP_DEBUG
-#define NLOSGR_DBG_ARG , long long& dbg_got, long long& dbg_win, long long& dbg_pass
-#define NLOSGR_DBG_PASS , dbg_got, dbg_win, dbg_pass
-#else
-#define NLOSGR_DBG_ARG
-#define NLOSGR_DBG_PASS
-#endif
-// Refill, issued one window ahead (its LDS reads overlap the window being computed): lanes free at
-// window Wn (fr) are assigned records of Wn's bucket, then of the kSLate buckets behind (late);
-// the bucket cursors advance now, the records land in (pid, pr) for sweep_commit.
-struct SweepPf {
-    bool pf, late;
-    int pid;
-    float4 pr;
-};
-__device__ __forceinline__ void sweep_issue(int Wn, bool fr, const float4* rec, const unsigned short* idx, int* bcur,
-                                            const int* bend, int nb, SweepPf& f) {
-    const int lane = lane_id();
-    f.pf = false; f.late = false; f.pid = 0;
-    const unsigned long long fm = __builtin_amdgcn_ballot_w64(fr);
-    const int nfree = __popcll(fm);
-    if (nfree == 0) return;
-    const int rank = lanes_below(fm);
-    const int bb = Wn / kSW;
-    int took = 0;
-    if (bb < nb) {
-        const int c0 = __builtin_amdgcn_readfirstlane(bcur[bb]);
-        const int c1 = __builtin_amdgcn_readfirstlane(bend[bb]);
-        const int k1 = min(nfree, c1 - c0);
-        if (k1 > 0) {
-            if (fr && rank < k1) { f.pid = idx[c0 + rank]; f.pf = true; }
-            if (lane == 0) bcur[bb] = c0 + k1;
-            took = k1;
-        }
-    }
-#pragma unroll
-    for (int back = 1; back <= kSLate; ++back) {
-        const int lb = bb - back;
-        if (took >= nfree || lb < 0) break;
-        if (lb >= nb) continue;
-        const int c0 = __builtin_amdgcn_readfirstlane(bcur[lb]);
-        const int c1 = __builtin_amdgcn_readfirstlane(bend[lb]);
-        const int k2 = min(nfree - took, c1 - c0);
-        if (k2 <= 0) continue;
-        if (fr && rank >= took && rank < took + k2) { f.pid = idx[c0 + rank - took]; f.pf = true; f.late = true; }
-        if (lane == 0) bcur[lb] = c0 + k2;
-        took += k2;
-    }
-    if (f.pf) f.pr = rec[f.pid];
-}
-
-// lane state of the sweep: the segment (ga, al, ks) on [kl, kh] and cc = 2^(2 ga)
-struct SweepLane {
-    bool busy;
-    float ga, al, ks, cc;
-    int kl, kh;
-    __device__ __forceinline__ void idle() { busy = false; ga = 0.f; al = -1000.f; ks = 0.f; cc = 1.f; kl = 0; kh = -1; }
-};
-
-// apply an issued refill at window Wn: eligible records start here (seeded at Wn <= kl); a late record
-// gives its remainder [Wn, kh] when that is at least a window long and leaves its head [kl, Wn - 1]
-// (or, when shorter, the whole record) for the next pass
-__device__ __forceinline__ void sweep_commit(int Wn, const SweepPf& f, float4* rec, unsigned short* hidx, int& nheads,
-                                             SweepLane& L) {
-    bool head = false;
-    if (f.pf) {
-        const int rkl = rec_kl(f.pr), rkh = rec_kh(f.pr);
-        if (!f.late || rkh >= Wn + kSW - 1) {
-            L.busy = true;
-            L.ga = f.pr.x; L.al = f.pr.y; L.ks = f.pr.z;
-            L.kl = f.late ? Wn : rkl;
-            L.kh = rkh;
-            L.cc = fast_exp2(2.f * L.ga);
-            if (f.late) rec[f.pid].w = rec_pack(rkl, Wn - 1);
-        }
-        head = f.late;
-    }
-    const unsigned long long hm = __builtin_amdgcn_ballot_w64(head);
-    if (head) hidx[nheads + lanes_below(hm)] = (unsigned short)f.pid;
-    nheads += __popcll(hm);
-    if (!L.busy) L.idle();
-}
-
-// sweep the batch rec[0..n) into the wave's histogram (see above); leaves the batch empty
-#ifdef NLOSGR_SWEEP_DEBUG
-#define NLOSGR_DBG_ARG , long long& dbg_got, long long& dbg_win, long long& dbg_pass
-#define NLOSGR_DBG_PASS , dbg_got, dbg_win, dbg_pass
-#else
-#define NLOSGR_DBG_ARG
-#define NLOSGR_DBG_PASS
-#endif
-__device__ void sweep_batch(float4* rec, unsigned short* idx, unsigned short* hidx, int* cnt, int* bcur, int* bend,
-                            float* hist, int n, int nb NLOSGR_DBG_ARG) {
-    const int lane = lane_id();
-    int nlist = n;
-    bool first = true;
-    while (nlist > 0) {
-        sweep_sort(rec, first ? nullptr : hidx, nlist, idx, cnt, bcur, bend, nb);
-        first = false;
-#ifdef NLOSGR_SWEEP_DEBUG
-        if (lane == 0) dbg_pass += 1;
-#endif
-        int nheads = 0;
-        SweepLane L;
-        L.idle();
-        SweepPf f;
-        int W = next_pending(bcur, bend, nb, 0) * kSW;
-        sweep_issue(W, true, rec, idx, bcur, bend, nb, f);
-        sweep_commit(W, f, rec, hidx, nheads, L);
-        while (true) {
-            if (!__builtin_amdgcn_ballot_w64(L.busy)) {   // every lane idle: jump to the next pending window
-                int nb2 = next_pending(bcur, bend, nb, W / kSW + 1);
-                if (nb2 < 0) nb2 = next_pending(bcur, bend, nb, 0);
-                if (nb2 < 0) break;
-                W = nb2 * kSW;
-                sweep_issue(W, true, rec, idx, bcur, bend, nb, f);
-                sweep_commit(W, f, rec, hidx, nheads, L);
-                continue;
-            }
-            // refill of the next window, issued now
-            sweep_issue(W + kSW, !(L.busy && L.kh >= W + kSW), rec, idx, bcur, bend, nb, f);
-            // the window: two exp2 seeds (W, W + 8), then value(t+1) = value(t) q, q *= cc on each half
-            const float ta = (float)W - L.ks, tb = ta + (float)(kSW / 2);
-            const float ea = fmaf(L.ga, ta * ta, L.al), eb = fmaf(L.ga, tb * tb, L.al);
-            float ca = fast_exp2(ea), qa = fast_exp2(L.ga * fmaf(2.f, ta, 1.f));
-            float cb = fast_exp2(eb), qb = fast_exp2(L.ga * fmaf(2.f, tb, 1.f));
-            float x[kSW];
-            const bool exact = L.busy && (ea < kSeedMin || eb < kSeedMin);
-            if (__builtin_amdgcn_ballot_w64(exact)) {
-                // a seed that would underflow (narrow Gaussian, W < kl): exact values of [kl, kh]
-#pragma unroll
-                for (int r = 0; r < kSW; ++r) {
-                    const float tr = ta + (float)r;
-                    const int bin = W + r;
-                    const float ve = (bin >= L.kl && bin <= L.kh) ? fast_exp2(fmaf(L.ga, tr * tr, L.al)) : 0.f;
-                    const float vr = r < kSW / 2 ? ca : cb;
-                    x[r] = exact ? ve : vr;
-                    if (r < kSW / 2) { ca *= qa; qa *= L.cc; } else { cb *= qb; qb *= L.cc; }
-                }
-            } else {
-#pragma unroll
-                for (int r = 0; r < kSW / 2; ++r) {
-                    x[r] = ca;
-                    x[r + kSW / 2] = cb;
-                    ca *= qa;
-                    cb *= qb;
-                    qa *= L.cc;
-                    qb *= L.cc;
-                }
-            }
-#ifdef NLOSGR_SWEEP_DEBUG
-            if (L.busy) {
-                const int lo = max(W, L.kl), hi = min(W + kSW - 1, L.kh);
-                if (hi >= lo) dbg_got += hi - lo + 1;
-            }
-            if (lane == 0) dbg_win += 1;
-#endif
-            const float s = window_reduce(x);
-            if ((lane & 3) == 0) {
-                float* h = hist + W + (lane >> 2);
-                *h += s;
-            }
-            W += kSW;
-            if (!(L.busy && L.kh >= W)) L.idle();
-            sweep_commit(W, f, rec, hidx, nheads, L);
-        }
-        wave_sync();
-        nlist = nheads;
-    }
-}
-
-template <int PRESET>
-__global__ __launch_bounds__(kBlock) void fwd_sweep_kernel(KArgs k) {
-    extern __shared__ __align__(16) float smem[];
-    const int nr = k.geo.nr, nt = k.geo.nt, np_ = k.geo.np;
-    const SweepLayout L(nr, nt, np_);
-    float2* tth = reinterpret_cast<float2*>(smem);
-    float2* tph = tth + nt;
-    const int wave = threadIdx.x >> 6, lane = lane_id();
-    float* wb = smem + wave * L.wave_stride;
-    float* hist = wb + L.hist;
-    unsigned* rayq = reinterpret_cast<unsigned*>(wb + L.ring);
-    float4* rec = reinterpret_cast<float4*>(wb + L.rec);
-    unsigned short* idx = reinterpret_cast<unsigned short*>(wb + L.idx);
-    unsigned short* hidx = reinterpret_cast<unsigned short*>(wb + L.hidx);
-    int* cnt = reinterpret_cast<int*>(wb + L.cnt);
-    int* bcur = reinterpret_cast<int*>(wb + L.bcur);
-    int* bend = reinterpret_cast<int*>(wb + L.bend);
-    const int nb = L.nb;
-    const int p = blockIdx.x;
-    const int gsplit = blockIdx.y, nsp = gridDim.y;
-    const int gper = (((k.g.ng + nsp - 1) / nsp) + 63) & ~63;
-    const int g_lo = gsplit * gper, g_hi = min(k.g.ng, g_lo + gper);
-
-    for (int t = threadIdx.x; t < nt; t += blockDim.x)
-        tth[t] = make_float2(k.geo.sin_theta[(size_t)p * nt + t], k.geo.cos_theta[(size_t)p * nt + t]);
-    for (int t = threadIdx.x; t < np_; t += blockDim.x)
-        tph[t] = make_float2(k.geo.cos_phi[(size_t)p * np_ + t], k.geo.sin_phi[(size_t)p * np_ + t]);
-    for (int t = lane; t < nb * kSW + kSW; t += 64) hist[t] = 0.f;
-    __syncthreads();
-
-    const float px = k.geo.wall[3 * p], py = k.geo.wall[3 * p + 1], pz = k.geo.wall[3 * p + 2];
-    const float* lin = k.geo.grid_lin + 4 * (size_t)p;
-    const float mc2 = k.opt.cutoff * k.opt.cutoff;
-    const float r0 = k.geo.r[0];
-    const float dr = nr > 1 ? (k.geo.r[nr - 1] - r0) / (float)(nr - 1) : 0.f;
-    const float inv_dr = dr > 0.f ? 1.0f / dr : 0.f;
-    int nrec = 0, qhead = 0, qcount = 0;
-#ifdef NLOSGR_SWEEP_DEBUG
-    long long dbg_got = 0, dbg_exp = 0, dbg_win = 0, dbg_pass = 0, dbg_batch = 0;
-#endif
-
-    for (int base = g_lo + wave * 64; base < g_hi; base += kBlock) {
-        Pair P;
-        float lw = 0.f;
-        bool more = false;
-        int ci = 0, cj = 0;
-        P.i0 = P.i1 = P.j0 = P.j1 = 0;
-        {
-            const int gi = base + lane;
-            const int gl = min(gi, k.g.ng - 1);
-            const GaussRec nrec_ = k.recs[gl];
-            if (gi < g_hi) {
-                float mu[3];
-                load_rec(nrec_, P, mu);
-                pair_setup<PRESET, false>(k, k.g.features + (size_t)gl * k.g.k_feat, mu, px, py, pz, lin, mc2, P);
-                more = (P.w > 0.f) && P.i0 <= P.i1 && P.j0 <= P.j1;
-                lw = more ? flog2(P.w) : 0.f;
-            }
-            ci = P.i0; cj = P.j0;
-        }
-        while (true) {
-            if (qcount < 64 && __builtin_amdgcn_ballot_w64(more)) {
-                wave_sync();
-                enumerate_box<false>(P.M, P.i1, P.j0, P.j1, more, ci, cj, tth, tph, nt - 1, rayq, qhead, qcount);
-                wave_sync();
-            }
-            const bool anymore = __builtin_amdgcn_ballot_w64(more) != 0;
-            if (qcount == 0) {
-                if (!anymore) break;
-                continue;
-            }
-            if (qcount < 64 && anymore) continue;
-            // queue entries -> segment records (lane = entry; pair data from lane `slot`)
-            const int ntake = min(64, qcount);
-            const bool take = lane < ntake;
-            const unsigned e = take ? rayq[(qhead + lane) & (kRQ - 1)] : 0u;
-            const int slot = e & 0xFF, i = (e >> 8) & 0xFFF, j = e >> 20;
-            float A[9], u0[3];
-#pragma unroll
-            for (int c = 0; c < 9; ++c) A[c] = __shfl(P.A[c], slot);
-#pragma unroll
-            for (int c = 0; c < 3; ++c) u0[c] = __shfl(P.u0[c], slot);
-            const float lws = __shfl(lw, slot);
-            bool ok = false;
-            Ray R;
-            const float2 th = tth[i], ph = tph[j];
-            if (take) ok = ray_setup<false>(A, u0, th.x * ph.x, th.x * ph.y, th.y, mc2, r0, inv_dr, nr, R);
-            qhead = (qhead + ntake) & (kRQ - 1);
-            qcount -= ntake;
-            const unsigned long long m = __builtin_amdgcn_ballot_w64(ok);
-#ifdef NLOSGR_SWEEP_DEBUG
-            if (ok) dbg_exp += R.kh - R.kl + 1;
-#endif
-            if (ok) {
-                const float ga = -kHalfLog2e * R.a * dr * dr;
-                const float al = fmaf(-kHalfLog2e, R.m2min, lws) + flog2(th.x);
-                rec[nrec + lanes_below(m)] = make_float4(ga, al, R.ks, rec_pack(R.kl, R.kh));
-            }
-            nrec += __popcll(m);
-            if (nrec > kSCap - 64) {
-                wave_sync();
-                sweep_batch(rec, idx, hidx, cnt, bcur, bend, hist, nrec, nb NLOSGR_DBG_PASS);
-#ifdef NLOSGR_SWEEP_DEBUG
-                dbg_batch += 1;
-#endif
-                nrec = 0;
-                wave_sync();
-            }
-        }
-    }
-    if (nrec > 0) {
-        wave_sync();
-        sweep_batch(rec, idx, hidx, cnt, bcur, bend, hist, nrec, nb NLOSGR_DBG_PASS);
-    }
-#ifdef NLOSGR_SWEEP_DEBUG
-    {
-        long long a = dbg_got, b = dbg_exp;
-        for (int o = 32; o > 0; o >>= 1) { a += __shfl_xor(a, o); b += __shfl_xor(b, o); }
-        if (lane == 0 && a != b && blockIdx.x < 64) printf("sweep dbg p %d split %d wave %d got %lld expect %lld\n", p, gsplit, wave, a, b);
-        if (lane == 0 && (blockIdx.x % 97) == 5)
-            printf("sweep eff p %d split %d wave %d slots %lld windows %lld eff %.3f passes %lld batches %lld\n", p, gsplit, wave,
-                   a, dbg_win, (double)a / (1024.0 * (double)(dbg_win > 0 ? dbg_win : 1)), dbg_pass, dbg_batch);
-    }
-#endif
-    __syncthreads();
-    if (k.hist_out) {
-        const float hs = k.geo.hscale[p];
-        for (int t = threadIdx.x; t < nr; t += blockDim.x) {
-            float s = 0.f;
-            for (int w = 0; w < kWaves; ++w) s += smem[w * L.wave_stride + L.hist + t];
-            if (nsp > 1)
-                k.hpart[((size_t)gsplit * k.geo.nwall + p) * nr + t] = s;
-            else
-                k.hist_out[(size_t)p * nr + t] = s * k.geo.att[t] * hs;
-        }
-    }
-}
-
 // Dense no-occlusion forward (cutoff <= 0: every Gaussian at every sample, the reference's own
 // support): every ray covers every bin, so the lane-serial drain above degenerates (all segments
 // claim the same bins; read-add-write chains bound by LDS latency).  Here lane = bin instead: a
@@ -1573,7 +1024,7 @@ __global__ __launch_bounds__(kBlock) void fwd_dense_kernel(KArgs k) {
     const FwdDenseLayout L(nr, nt, np_);
     float2* tth = reinterpret_cast<float2*>(smem);
     float2* tph = tth + nt;
-    const int wave = threadIdx.x >> 6, lane = lane_id();
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = lane_id();   // wave-uniform (SGPR)
     float4* rp = reinterpret_cast<float4*>(smem + L.rays) + wave * 64;
     const int p = blockIdx.x;
     const int gsplit = blockIdx.y, nsp = gridDim.y;
@@ -1703,6 +1154,9 @@ constexpr int kBSteps = NLOSGR_BSTEPS;   // bins per lane per backward drain rou
 #define NLOSGR_BPREFIX 1   // no-occlusion culled backward: moments by nested running sums (see bwd_kernel)
 #endif
 #ifndef NLOSGR_BSTEPS_TAIL
+// (round 4's 40-bin rounds spilled 36 B per lane, reloaded and re-stored every wall point: ~1.2 GB of
+// scratch writes per launch reached HBM.  The wave index read as an SGPR (readfirstlane) keeps the
+// wave-derived LDS bases out of VGPRs and the kernel spill-free at 40; 32 bins cost ~30 ms per step)
 #define NLOSGR_BSTEPS_TAIL 40
 #endif
 // the staged gradient row is zero-padded by the longest round (no-occlusion TAIL rounds)
@@ -1886,7 +1340,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
     const int nr = k.geo.nr, nt = k.geo.nt, np_ = k.geo.np;
     constexpr bool shr = SHR;   // == (k.bshared != 0)
     const BwdLayout L(nr, nt, np_, shr);
-    const int wave = threadIdx.x >> 6, lane = lane_id();
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = lane_id();   // wave-uniform (SGPR)
     float* wb = smem + L.wave_base + wave * L.wave_stride;
     float* gbase = shr ? smem : wb;
     float* grow = gbase + L.grow;
@@ -2620,13 +2074,6 @@ void launch_fwd(const KArgs& ka, size_t shm, hipStream_t s) {
     const char* ftail = getenv("NLOSGR_FTAIL");
     const bool tail = kCanTail && ka.opt.cutoff >= kTailCutoff && (!ka.counts || NLOSGR_FCOUNT_ON) && !(ftail && ftail[0] == '0') &&
                       (MODE != NLOSGR_MODE_NETF || ka.opt.c_deltaT <= kSmallX);
-    // NLOSGR_FSWEEP=1: the window sweep instead of the lane-serial TAIL drain (experimental; A/B)
-    const char* fsw = getenv("NLOSGR_FSWEEP");
-    const size_t shs = (size_t)SweepLayout(ka.geo.nr, ka.geo.nt, ka.geo.np).total * sizeof(float);
-    if (tail && MODE == NLOSGR_MODE_NOOCL && !CACHE && (fsw && fsw[0] == '1') && shs <= 160 * 1024) {
-        hipLaunchKernelGGL((fwd_sweep_kernel<PRESET>), grid, dim3(kBlock), shs, s, ka);
-        return;
-    }
     if (tail) hipLaunchKernelGGL((fwd_kernel<PRESET, MODE, DENSE, RAYS, CACHE, kCanTail>), grid, dim3(kBlock), shm, s, ka);
     else hipLaunchKernelGGL((fwd_kernel<PRESET, MODE, DENSE, RAYS, CACHE>), grid, dim3(kBlock), shm, s, ka);
 }
@@ -2708,9 +2155,8 @@ size_t fpart_bytes(const nlosgr_gaussians* g, const nlosgr_geometry* geo) {
 bool fx_eligible(const nlosgr_options* opt, bool dense, bool rays, bool counts, bool hist, bool cache) {
     const char* e = getenv("NLOSGR_FFX");
     const char* ft = getenv("NLOSGR_FTAIL");
-    const char* fsw = getenv("NLOSGR_FSWEEP");
     return opt->mode == NLOSGR_MODE_NOOCL && opt->cutoff >= kTailCutoff && !dense && !rays && !counts && hist && !cache &&
-           !(e && e[0] == '0') && !(ft && ft[0] == '0') && !(fsw && fsw[0] == '1');
+           !(e && e[0] == '0') && !(ft && ft[0] == '0');
 }
 // after the ray cache: drho [P][ng] | sh partials [nsh][ng][kShPart] | 256-B diagnostics tail |
 // forward split partial histograms [nfsplit][P][nr]
@@ -2767,7 +2213,7 @@ int run_fwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_
         launch_preprocess(g, (GaussRec*)workspace, s);
         HIPCHK(hipGetLastError());
     }
-    const size_t shm = (size_t)FwdLayout(geo->nr, geo->nt, geo->np).total * sizeof(float);
+    const size_t shm = (size_t)FwdLayout(geo->nr, geo->nt, geo->np, fx).total * sizeof(float);
     // NLOSGR_FDREG=0 routes the dense histogram through fwd_kernel instead (parity cross-check in tests)
     const char* fdreg = getenv("NLOSGR_FDREG");
     if (dense && !rays && !counts && hist_out && opt->mode == NLOSGR_MODE_NOOCL && geo->nr <= 1024 &&

@@ -35,6 +35,9 @@ for flags in (0, 4, 1, 2):
     render_forward(*args, cfg); torch.cuda.synchronize()
     t0 = time.perf_counter(); render_forward(*args, cfg); torch.cuda.synchronize()
     res[flags] = (time.perf_counter() - t0) * 1000
+if os.environ.get("NLOSGR_ABLATE_FWD_ONLY") == "1":
+    print(json.dumps({'config': cfgname, 'mode': mode, 'cutoff': cutoff, 'fwd_ms_by_flags': res}))
+    sys.exit(0)
 cache = os.environ.get("NLOSGR_ABLATE_CACHE", "1") == "1"
 hist, _, ws = render_forward(*args, base, ray_cache=True)
 grad = torch.randn_like(hist) * 1e-3

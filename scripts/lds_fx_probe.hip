@@ -9,6 +9,10 @@
 //   mode 4: ds_add_u64 packed, starts within 12 bins of a wave base (heavy clustering)
 //   mode 5: float2 read-add-write, starts within 12 bins of a wave base
 //   mode 6: ds_add_u64 packed, distinct consecutive pairs (lane l at base + 2l: conflict-free)
+//   mode 7: as mode 1 with only lanes 0-31 active (does a masked lane cost LDS cycles?)
+//   mode 8: as mode 1 with every other lane active (32 active, all four 16-lane groups busy)
+//   mode 9: as mode 6 with lanes 0-31 active
+//   mode 10: ds_add_f32 (no return) at random bins, one bin per op (build with -munsafe-fp-atomics)
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdint.h>
@@ -23,7 +27,7 @@ constexpr int kBins = 1024, kSteps = 20, kIters = 2000, kBlocks = 256 * 12;
 
 template <int MODE>
 __global__ __launch_bounds__(256) void bench(float* out, int seed) {
-    constexpr bool ATOM = MODE == 1 || MODE == 3 || MODE == 4 || MODE == 6;
+    constexpr bool ATOM = MODE == 1 || MODE == 3 || MODE == 4 || (MODE >= 6 && MODE != 10);
     constexpr int SPREAD = (MODE == 2 || MODE == 3) ? 48 : ((MODE == 4 || MODE == 5) ? 12 : 0);
     __shared__ __align__(16) unsigned h32[4 * (kBins + 192)];
     for (int t = threadIdx.x; t < 4 * (kBins + 192); t += 256) h32[t] = 0u;
@@ -35,7 +39,7 @@ __global__ __launch_bounds__(256) void bench(float* out, int seed) {
     for (int it = 0; it < kIters; ++it) {
         st = st * 1664525u + 1013904223u;
         int pos;
-        if (MODE == 6) {
+        if (MODE == 6 || MODE == 9) {
             pos = (int)(__builtin_amdgcn_readfirstlane((st >> 8) % (kBins - 160)) & ~1) + 2 * lane;
         } else if (SPREAD) {
             const unsigned b = __builtin_amdgcn_readfirstlane((st >> 8) % (kBins - kSteps - SPREAD));
@@ -43,7 +47,12 @@ __global__ __launch_bounds__(256) void bench(float* out, int seed) {
         } else {
             pos = (int)((st >> 8) % (kBins - kSteps)) & ~1;
         }
-        if (!ATOM) {
+        if (MODE == 10) {
+            float* hf = reinterpret_cast<float*>(h32) + wbase + pos;
+#pragma unroll
+            for (int m = 0; m < kSteps / 2; ++m)
+                __hip_atomic_fetch_add(hf + 2 * m, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        } else if (!ATOM) {
             float2* hb = reinterpret_cast<float2*>(reinterpret_cast<float*>(h32) + wbase + pos);
 #pragma unroll
             for (int m = 0; m < kSteps / 2; ++m) {
@@ -52,6 +61,8 @@ __global__ __launch_bounds__(256) void bench(float* out, int seed) {
                 hb[m] = x;
                 __asm__ __volatile__("" ::: "memory");
             }
+        } else if ((MODE == 7 || MODE == 9) && lane >= 32) {
+        } else if (MODE == 8 && (lane & 1)) {
         } else {
             unsigned long long* hb = reinterpret_cast<unsigned long long*>(h32 + wbase + pos);
 #pragma unroll
@@ -87,7 +98,7 @@ void run(float* d) {
 int main() {
     float* d;
     hipMalloc(&d, kBlocks * 256 * sizeof(float));
-    run<0>(d); run<1>(d); run<2>(d); run<3>(d); run<4>(d); run<5>(d); run<6>(d);
+    run<0>(d); run<1>(d); run<2>(d); run<3>(d); run<4>(d); run<5>(d); run<6>(d); run<7>(d); run<8>(d); run<9>(d); run<10>(d);
     hipFree(d);
     return 0;
 }
