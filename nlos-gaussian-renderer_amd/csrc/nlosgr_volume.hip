@@ -480,11 +480,73 @@ __device__ __forceinline__ int fx_exponent(unsigned amax_bits) {
     e = kFxBits - e;
     return e < -120 ? -120 : (e > 120 ? 120 : e);
 }
+// FX bank placement.  A ds_add_u64 is serviced in 4 groups of 16 lanes; two lanes of a group whose words lie
+// on the same bank pair (word index mod 16) serialize.  Every active lane advances 10 words per round, so the
+// pairs' residues within a group stay fixed for a segment's life: at refill a new segment may start up to
+// kFxShift words (2 bins each) early, on the nearest residue no older lane of its group holds and no lower
+// new lane of the group takes (3 claim rounds of row-wide DPP ORs; a segment that finds none keeps its
+// start).  The early bins get the Gaussian's exact values (as the TAIL overrun past the end), only while the
+// recurrence's seed stays >= 2^-100 units.  Placement never affects correctness, only conflicts.
+#ifndef NLOSGR_FXSHIFT
+#define NLOSGR_FXSHIFT 4
+#endif
+constexpr int kFxShift = NLOSGR_FXSHIFT;
+template <int CTRL>
+__device__ __forceinline__ unsigned dpp_u(unsigned v) {
+    return (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, true);
+}
+__device__ __forceinline__ unsigned row_or(unsigned x) {   // OR over the lane's 16-lane row
+    x |= dpp_u<0x121>(x);   // row_ror:1
+    x |= dpp_u<0x122>(x);   // row_ror:2
+    x |= dpp_u<0x124>(x);   // row_ror:4
+    x |= dpp_u<0x128>(x);   // row_ror:8
+    return x;
+}
+__device__ __forceinline__ unsigned row_or_below(unsigned x) {   // OR over the lanes below in the row
+    x |= dpp_u<0x111>(x);   // row_shr:1 (lanes shifted in read 0)
+    x |= dpp_u<0x112>(x);
+    x |= dpp_u<0x114>(x);
+    x |= dpp_u<0x118>(x);
+    return dpp_u<0x111>(x);
+}
+
 // round to nearest (floor(x + 0.5)) as an integer in one VALU instruction; 0 <= x < 2^31
 __device__ __forceinline__ unsigned cvt_rpi(float x) {
     int r;
     __asm__("v_cvt_rpi_i32_f32 %0, %1" : "=v"(r) : "v"(x));
     return (unsigned)r;
+}
+
+// FX refill placement (see kFxShift): newl = this lane took a new segment, act = it holds one
+__device__ __forceinline__ void fx_place(bool newl, bool act, Drain& d) {
+    if (!__builtin_amdgcn_ballot_w64(newl)) return;
+    const int pb = d.pos >> 1, ph = pb & 15, o = d.pos & 1;
+    unsigned occ = row_or((act && !newl) ? (1u << ph) : 0u);
+    // reach: the seed exponent at the new start stays >= -100 (no flush to zero), the start >= bin 0
+    const float span = d.al + 100.f;
+    const float tm = span > 0.f ? __builtin_amdgcn_sqrtf(span * __builtin_amdgcn_rcpf(fmaxf(-d.ga, 1e-30f))) : 0.f;
+    const int smax = newl ? min(min(kFxShift, pb), (int)floorf(0.5f * (d.t - (float)o + tm))) : -1;
+    bool pend = newl && smax >= 0;
+    int sh = 0;
+#pragma unroll
+    for (int it = 0; it < 3; ++it) {
+        const unsigned fm = ~occ & 0xFFFFu;
+        const unsigned x = ((fm << (15 - ph)) | (fm >> (ph + 1))) & 0xFFFFu;   // bit 15 - k = residue ph - k
+        const int dd = x ? (int)__builtin_clz(x) - 16 : 16;
+        const bool want = pend && dd <= smax;
+        const unsigned bit = want ? 1u << ((ph - dd) & 15) : 0u;
+        const bool won = want && !(row_or_below(bit) & bit);
+        if (won) sh = dd;
+        pend = pend && want && !won;
+        occ |= row_or(won ? bit : 0u);
+        if (!__builtin_amdgcn_ballot_w64(pend)) break;
+    }
+    if (sh > 0) {
+        const int delta = o + 2 * sh;
+        d.pos -= delta;
+        d.rem += delta;
+        d.t -= (float)delta;
+    }
 }
 
 template <int PRESET, int MODE, bool DENSE, bool RAYS, bool CACHE, bool TAIL = false, bool FX = false>
@@ -617,6 +679,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
                 const int ntake = min(nidle, qcount);
                 qhead = (qhead + ntake) & (kRQ - 1);
                 qcount -= ntake;
+                if (FX && kFxShift > 0) fx_place(take && act, act, d);
             }
             const bool anyact = __builtin_amdgcn_ballot_w64(act) != 0;
             if (!anyact) {
