@@ -516,6 +516,21 @@ __device__ __forceinline__ unsigned cvt_rpi(float x) {
     __asm__("v_cvt_rpi_i32_f32 %0, %1" : "=v"(r) : "v"(x));
     return (unsigned)r;
 }
+// two bins of a TAIL drain round into the wave's LDS histogram: FX = one packed fixed-point ds_add_u64
+// (values in units), otherwise a float2 read-add-write (the claim table keeps the lanes' pairs distinct)
+template <bool FX>
+__device__ __forceinline__ void emit2(float2* at, float v0, float v1) {
+    if (FX) {
+        const unsigned long long pv = ((unsigned long long)cvt_rpi(v1) << 32) | cvt_rpi(v0);
+        __hip_atomic_fetch_add(reinterpret_cast<unsigned long long*>(at), pv, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WAVEFRONT);
+    } else {
+        float2 x = *at;
+        x.x += v0; x.y += v1;
+        *at = x;
+        __asm__ __volatile__("" ::: "memory");
+    }
+}
 
 // FX refill placement (see kFxShift): newl = this lane took a new segment, act = it holds one
 __device__ __forceinline__ void fx_place(bool newl, bool act, Drain& d) {
@@ -554,7 +569,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
     extern __shared__ __align__(16) float smem[];
     const int nr = k.geo.nr, nt = k.geo.nt, np_ = k.geo.np;
     const FwdLayout L(nr, nt, np_, FX);
-    static_assert(!FX || (TAIL && MODE == NLOSGR_MODE_NOOCL && !DENSE && !RAYS), "fixed-point drain: TAIL no-occlusion histogram");
+    static_assert(!FX || (TAIL && !DENSE && !RAYS), "fixed-point drain: TAIL histogram drains only");
     float2* tth = reinterpret_cast<float2*>(smem);
     float2* tph = tth + nt;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = lane_id();   // wave-uniform (SGPR)
@@ -589,6 +604,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
     const int flags = k.opt.flags;
     // FX: log2 of the unit scale, folded into every pair's log2 amplitude; per-lane peak bookkeeping
     const float fxE = FX ? (float)fx_exponent(*k.fx_amax) : 0.f;
+    const float fxS = FX ? fast_exp2(fxE) : 1.f;   // exact: fxE is an integer
     float fthr = kFxLimit / 64.f;   // wave-uniform
     float fpk = 0.f, fxs = 0.f;     // this lane's segment peak, and its peaks since the last check
     unsigned* hist32 = reinterpret_cast<unsigned*>(hist);
@@ -631,7 +647,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
                 more = (P.w > 0.f) && P.i0 <= P.i1 && P.j0 <= P.j1;
                 lw = more ? flog2(P.w) + fxE : 0.f;
                 sc = P.sigma * cdt;
-                wc = more ? P.w * cdt : 0.f;
+                wc = more ? P.w * cdt * fxS : 0.f;   // netf: the value's scale rides on T
             }
             if (flags & 2) more = false;      // diagnostics: pair setup only
             npair += NLOSGR_FCOUNT_ON ? 0u : (unsigned)__builtin_popcountll(__builtin_amdgcn_ballot_w64(more));
@@ -671,7 +687,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
                     if (MODE == NLOSGR_MODE_NETF && TAIL && QUADF) d.T *= d.wc;   // the weight rides on T
                     act = got && !(flags & 4);    // diagnostics: segment records only
                     if (FX && act) {
-                        fpk = fast_exp2(d.al);    // the segment's largest value (t = 0), in units
+                        // the segment's largest value (t = 0), in units (netf: T <= its start x (1 + 1e-7)^nr)
+                        fpk = MODE == NLOSGR_MODE_NETF ? d.T * fast_exp2(d.al) * 1.001f
+                                                       : fast_exp2(d.al) * (MODE == NLOSGR_MODE_BININT ? 1.001f : 1.f);
                         fxs += fpk;
                     }
                 }
@@ -679,7 +697,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
                 const int ntake = min(nidle, qcount);
                 qhead = (qhead + ntake) & (kRQ - 1);
                 qcount -= ntake;
-                if (FX && kFxShift > 0) fx_place(take && act, act, d);
+                // (netf keeps its start: its transmittance would have to be re-seeded)
+                if (FX && kFxShift > 0 && MODE != NLOSGR_MODE_NETF) fx_place(take && act, act, d);
             }
             const bool anyact = __builtin_amdgcn_ballot_w64(act) != 0;
             if (!anyact) {
@@ -737,29 +756,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
                 // per-step mask switching).
                 const int o = d.pos & (VW - 1);
                 const int lim = remw + o;   // slot j is in the segment iff o <= j < lim
-                if (FX && win) {
-                    // fixed point: the same values as below, rounded to units, two bins per ds_add_u64
-                    float cur = fast_exp2(fmaf(d.ga, t * t, d.al));
-                    float q = fast_exp2(d.ga * fmaf(2.f, t, 1.f));
-                    const float cc = fast_exp2(2.f * d.ga);
-                    unsigned long long* hb8 = reinterpret_cast<unsigned long long*>(hb);
-#pragma unroll
-                    for (int kv = 0; kv < kSteps / VW; ++kv) {
-                        const float v0 = (kv == 0 && o) ? 0.f : cur;
-                        if (kv == 0) {
-                            cur = o ? cur : cur * q;
-                            q = o ? q : q * cc;
-                        } else {
-                            cur *= q;
-                            q *= cc;
-                        }
-                        const float v1 = cur;
-                        cur *= q;
-                        q *= cc;
-                        const unsigned long long pv = ((unsigned long long)cvt_rpi(v1) << 32) | cvt_rpi(v0);
-                        __hip_atomic_fetch_add(hb8 + kv, pv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-                    }
-                } else if (TAIL && win && MODE == NLOSGR_MODE_NOOCL) {
+                if (TAIL && win && MODE == NLOSGR_MODE_NOOCL) {
                     // the recurrence is seeded at pos (inside the support: a seed one bin further out can
                     // underflow for Gaussians much narrower than a bin); slot 0 before pos (o = 1) adds 0
                     float cur = fast_exp2(fmaf(d.ga, t * t, d.al));
@@ -779,10 +776,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
                         const float v1 = cur;
                         cur *= q;
                         q *= cc;
-                        float2 x = hb2[kv];
-                        x.x += v0; x.y += v1;
-                        hb2[kv] = x;
-                        compiler_fence();
+                        emit2<FX>(hb2 + kv, v0, v1);
                     }
                 } else if (TAIL && win && MODE == NLOSGR_MODE_BININT) {
                     // bin-integrated (C4), TAIL: the average of exp(-beta^2 t^2) over the bin [t - 1/2, t + 1/2]
@@ -824,10 +818,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
                             cur = pre ? cur : cur * q;
                             q = pre ? q : q * cc;
                         }
-                        float2 x = hb2[kv];
-                        x.x += v[0]; x.y += v[1];
-                        hb2[kv] = x;
-                        compiler_fence();
+                        emit2<FX>(hb2 + kv, v[0], v[1]);
                     }
                 } else if (TAIL && win) {
                     // netf, TAIL: out_k = w c dT sin(theta) pdf_k T_k, T_{k+1} = T_k (exp(-sigma pdf_k c dT)
@@ -861,10 +852,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
                         }
                         const float v1 = T * p1;
                         T *= fast_exp2(p1 * nsc) + 1e-7f;
-                        float2 x = hb2[kv];
-                        x.x += v0; x.y += v1;
-                        hb2[kv] = x;
-                        compiler_fence();
+                        emit2<FX>(hb2 + kv, v0, v1);
                     }
                 } else if (win) {
                     float cur = fast_exp2(fmaf(d.ga, t * t, d.al));
@@ -1029,7 +1017,7 @@ __global__ __launch_bounds__(kBlock) void hist_reduce_kernel(const float* __rest
 // (Cauchy-Schwarz with sum_m Y_lm(d)^2 = (2l+1)/4pi on the unit sphere; 5 % margin for the cuda preset's
 // eps-shortened view direction), as float bits (non-negative floats order like their bits)
 template <int PRESET>
-__global__ __launch_bounds__(kBlock) void fx_amax_kernel(nlosgr_gaussians g, unsigned* amax) {
+__global__ __launch_bounds__(kBlock) void fx_amax_kernel(nlosgr_gaussians g, float ascale, unsigned* amax) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     float a = 0.f;
     if (i < g.ng) {
@@ -1042,7 +1030,7 @@ __global__ __launch_bounds__(kBlock) void fx_amax_kernel(nlosgr_gaussians g, uns
             for (int c = l * l; c < (l + 1) * (l + 1) && c < g.k_feat; ++c) n2 += f[c] * f[c];
             sh += sqrtf(n2) * sqrtf((2.0f * l + 1.0f) * (0.25f / kPi));
         }
-        a = sig * (0.5f + 1.05f * sh) * 1.001f;
+        a = sig * (0.5f + 1.05f * sh) * 1.001f * ascale;   // ascale: the mode's factor (netf: c dT)
         if (!(a >= 0.f)) a = __uint_as_float(0x7f800000u);   // NaN parameters: E = 0
     }
     unsigned b = __float_as_uint(a);
@@ -2124,7 +2112,8 @@ int bwd_nsplit_ws(const nlosgr_gaussians* g, const nlosgr_geometry* geo0, const 
 template <int PRESET, int MODE, bool DENSE, bool RAYS, bool CACHE>
 void launch_fwd(const KArgs& ka, size_t shm, hipStream_t s) {
     const dim3 grid(ka.geo.nwall, (ka.hpart || ka.hfx) ? ka.nfsplit : 1);
-    if constexpr (MODE == NLOSGR_MODE_NOOCL && !DENSE && !RAYS && !CACHE) {
+    if constexpr ((MODE == NLOSGR_MODE_NOOCL || MODE == NLOSGR_MODE_NETF || MODE == NLOSGR_MODE_BININT) && !DENSE &&
+                  !RAYS && !CACHE) {
         if (ka.hfx) {   // run_fwd decided the fixed-point TAIL drain (fx_eligible)
             hipLaunchKernelGGL((fwd_kernel<PRESET, MODE, DENSE, RAYS, CACHE, true, true>), grid, dim3(kBlock), shm, s, ka);
             return;
@@ -2218,7 +2207,9 @@ size_t fpart_bytes(const nlosgr_gaussians* g, const nlosgr_geometry* geo) {
 bool fx_eligible(const nlosgr_options* opt, bool dense, bool rays, bool counts, bool hist, bool cache) {
     const char* e = getenv("NLOSGR_FFX");
     const char* ft = getenv("NLOSGR_FTAIL");
-    return opt->mode == NLOSGR_MODE_NOOCL && opt->cutoff >= kTailCutoff && !dense && !rays && !counts && hist && !cache &&
+    const bool mode_ok = opt->mode == NLOSGR_MODE_NOOCL || opt->mode == NLOSGR_MODE_BININT ||
+                         (opt->mode == NLOSGR_MODE_NETF && opt->c_deltaT <= kSmallX);   // (the TAIL drains)
+    return mode_ok && opt->cutoff >= kTailCutoff && !dense && !rays && !counts && hist && !cache &&
            !(e && e[0] == '0') && !(ft && ft[0] == '0');
 }
 // after the ray cache: drho [P][ng] | sh partials [nsh][ng][kShPart] | 256-B diagnostics tail |
@@ -2263,10 +2254,11 @@ int run_fwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_
         HIPCHK(hipMemsetAsync(ka.hfx, 0, (size_t)geo->nwall * geo->nr * sizeof(unsigned long long), s));
         HIPCHK(hipMemsetAsync(amax, 0, sizeof(unsigned), s));
         const int nb = (g->ng + kBlock - 1) / kBlock;
+        const float ascale = opt->mode == NLOSGR_MODE_NETF ? opt->c_deltaT : 1.0f;
         if (g->preset == NLOSGR_PRESET_TORCH)
-            hipLaunchKernelGGL(fx_amax_kernel<NLOSGR_PRESET_TORCH>, dim3(nb), dim3(kBlock), 0, s, *g, amax);
+            hipLaunchKernelGGL(fx_amax_kernel<NLOSGR_PRESET_TORCH>, dim3(nb), dim3(kBlock), 0, s, *g, ascale, amax);
         else
-            hipLaunchKernelGGL(fx_amax_kernel<NLOSGR_PRESET_CUDA>, dim3(nb), dim3(kBlock), 0, s, *g, amax);
+            hipLaunchKernelGGL(fx_amax_kernel<NLOSGR_PRESET_CUDA>, dim3(nb), dim3(kBlock), 0, s, *g, ascale, amax);
         HIPCHK(hipGetLastError());
     } else if (hist_out && nfs > 1 && g->ng > 0) {
         ka.hpart = (float*)fpart;
