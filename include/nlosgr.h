@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define NLOSGR_ABI_VERSION 6
+#define NLOSGR_ABI_VERSION 7
 
 /* convention presets */
 enum {
@@ -142,6 +142,8 @@ NLOSGR_API size_t nlosgr_workspace_bytes(const nlosgr_gaussians* g, const nlosgr
  * They set the workspace layout: change them only while no workspace sized under the old values is
  * still in use (a ray-cache backward must run under the forward's budgets). */
 NLOSGR_API void nlosgr_set_batch_budgets(double drho_mb, double tile_hpart_mb);
+/* The batch budgets in effect (MiB): lets a caller restore exactly what it changed. */
+NLOSGR_API void nlosgr_get_batch_budgets(double* drho_mb, double* tile_hpart_mb);
 
 /* Forward.  hist_out [P,nr] (may be NULL):  hscale[p]*att[k]*sum_{g,i,j} w_g(p) sin(theta_i) pdf
  *           ray_out  [P,nt*np,nr] (may be NULL, caller zero-fills): ray_scale*sum_g w_g(p) pdf,

@@ -2346,6 +2346,12 @@ void nlosgr_set_batch_budgets(double drho_mb, double tile_hpart_mb) {
     if (tile_hpart_mb > 0.0) b.tile_hpart_mb = tile_hpart_mb;
 }
 
+void nlosgr_get_batch_budgets(double* drho_mb, double* tile_hpart_mb) {
+    const BatchBudgets& b = batch_budgets();
+    if (drho_mb) *drho_mb = b.drho_mb;
+    if (tile_hpart_mb) *tile_hpart_mb = b.tile_hpart_mb;
+}
+
 const char* nlosgr_last_error(void) { return g_err; }
 
 size_t nlosgr_workspace_bytes(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_options* opt) {

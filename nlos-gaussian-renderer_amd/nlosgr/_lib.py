@@ -59,13 +59,13 @@ class AdamGroup(ctypes.Structure):
 
 ADAM_MAX_GROUPS = 8  # NLOSGR_ADAM_MAX_GROUPS
 MAX_PER_RAY = 256   # NLOSGR_MAX_PER_RAY
-ABI_VERSION = 6     # NLOSGR_ABI_VERSION
+ABI_VERSION = 7     # NLOSGR_ABI_VERSION
 
 # every symbol include/nlosgr.h declares (tests check the exports against this list)
 EXPORTS = ["nlosgr_workspace_bytes", "nlosgr_render_fwd", "nlosgr_render_bwd", "nlosgr_count_support",
            "nlosgr_bboxes", "nlosgr_rays_workspace_bytes", "nlosgr_filter_rays", "nlosgr_rays_fwd",
            "nlosgr_rays_bwd", "nlosgr_rays_analytic", "nlosgr_mse_workspace_bytes", "nlosgr_mse", "nlosgr_adam",
-           "nlosgr_carve_votes", "nlosgr_set_batch_budgets", "nlosgr_last_error", "nlosgr_abi_version"]
+           "nlosgr_carve_votes", "nlosgr_set_batch_budgets", "nlosgr_get_batch_budgets", "nlosgr_last_error", "nlosgr_abi_version"]
 
 _lib = None
 _load_error = None
@@ -114,6 +114,8 @@ def load():
     lib.nlosgr_bboxes.restype = ctypes.c_int
     lib.nlosgr_set_batch_budgets.argtypes = [ctypes.c_double, ctypes.c_double]
     lib.nlosgr_set_batch_budgets.restype = None
+    lib.nlosgr_get_batch_budgets.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
+    lib.nlosgr_get_batch_budgets.restype = None
     lib.nlosgr_last_error.argtypes = []
     lib.nlosgr_last_error.restype = ctypes.c_char_p
     lib.nlosgr_abi_version.argtypes = []
@@ -156,8 +158,9 @@ class batch_budgets:
         self.new = (drho_mb, tile_hpart_mb)
 
     def __enter__(self):
-        env = lambda k: float(os.environ.get(k, "0") or 0) or 1024.0
-        self.old = (env("NLOSGR_DRHO_MB"), env("NLOSGR_TILE_HPART_MB"))
+        d, h = ctypes.c_double(0.0), ctypes.c_double(0.0)
+        load().nlosgr_get_batch_budgets(ctypes.byref(d), ctypes.byref(h))   # the values in effect
+        self.old = (d.value, h.value)
         load().nlosgr_set_batch_budgets(*(float(v) if v is not None else -1.0 for v in self.new))
         return self
 

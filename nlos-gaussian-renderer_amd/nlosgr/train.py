@@ -265,6 +265,7 @@ class TrainStep:
         self.buckets = int(buckets)   # gradient all-reduce buckets overlapped with the backward (world > 1)
         self.iteration = 0
         self._batch_events = []
+        self._occl_plan = None           # occlusion mode: wall-point batches, planned at the first step
         # the slab orders' axis comes from the whole wall's centroid (the same on every rank)
         self.wall_c = wall_centroid(geo.wall, group) if self.world > 1 else wall_centroid(geo.wall)
         ng = model._mu.shape[0]
@@ -278,6 +279,7 @@ class TrainStep:
         the step count is kept."""
         m = self.model
         ng = m._mu.shape[0]
+        self._occl_plan = None
         self._tensors = [m._mu.data, m._features_dc.data.view(ng, -1), m._features_rest.data.view(ng, -1),
                          m._opacity.data.view(ng), m._scaling.data, m._rotation.data]
         step_count = self.adam.step_count
@@ -296,18 +298,26 @@ class TrainStep:
         return [mu_lr, o.feature_lr, o.feature_lr / 20.0, o.opacity_lr, o.scaling_lr, o.rotation_lr]
 
     def occl_batches(self):
-        """Wall-point ranges [p0, p1) of the occlusion mode's fused batches (row cache <= OCCL_BATCH_BYTES)."""
+        """Wall-point ranges [p0, p1) of the occlusion mode's fused batches (row cache <= OCCL_BATCH_BYTES).
+        Planned once (and again after rebind()), so the batch split, hence the summation order and the
+        cached/recompute choice, is the same every step."""
+        if self._occl_plan is not None:
+            return self._occl_plan
         P = self.geo.nwall
         per = max(1, tile_rows_bytes(self.geo) // max(1, P))
         budget = OCCL_BATCH_BYTES
         if self.geo.wall.is_cuda:
-            # at most half the free device memory (the batch's row cache is allocated per batch); when
-            # not even one wall point's rows fit, the backward recomputes the forward sweep instead
-            free, _ = torch.cuda.mem_get_info(self.geo.wall.device)
+            # at most half the free device memory (the batch's row cache is allocated per batch), counting
+            # the blocks the caching allocator holds but no tensor uses; when not even one wall point's
+            # rows fit, the backward recomputes the forward sweep instead
+            dev = self.geo.wall.device
+            free, _ = torch.cuda.mem_get_info(dev)
+            free += torch.cuda.memory_reserved(dev) - torch.cuda.memory_allocated(dev)
             budget = min(budget, free // 2)
         self._occl_cache = budget >= per
         nb = max(1, budget // per)
-        return [(p0, min(P, p0 + nb)) for p0 in range(0, P, nb)]
+        self._occl_plan = [(p0, min(P, p0 + nb)) for p0 in range(0, P, nb)]
+        return self._occl_plan
 
     def phase_ms(self):
         """(forward, backward) milliseconds of the last step from its HIP events (after a synchronize);

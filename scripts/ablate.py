@@ -26,7 +26,7 @@ f = features_flat(m).detach()
 args = (m._mu.detach(), m._scaling.detach(), m._rotation.detach(), m._opacity.detach(), f, geo)
 if os.environ.get('NLOSGR_ABLATE_ORDER') == 'slab':   # the Gaussian order TrainStep hands the backward
     from nlosgr.train import slab_order
-    perm = slab_order(args[0], geo.wall)
+    perm = slab_order(args[0], geo.wall, size=args[1].max(1).values)
     args = tuple(t[perm].contiguous() for t in args[:5]) + (geo,)
 base = make_config(m, scene, preset, mode, cutoff=cutoff)
 res = {}

@@ -125,3 +125,29 @@ def test_occl_row_cache_size_matches_library(nwall, nt, np_, nr):
     assert sizes[0] > 0, lib.nlosgr_last_error()
     want = tile_rows_bytes(SimpleNamespace(nwall=nwall, nt=nt, np=np_, nr=nr))
     assert sizes[1] - sizes[0] == (want + 255) // 256 * 256
+
+
+def test_batch_budgets_restore_the_values_in_effect():
+    """batch_budgets restores the budgets that were in effect (nlosgr_get_batch_budgets),
+    not the environment's defaults, so nested contexts and direct nlosgr_set_batch_budgets calls survive."""
+    from nlosgr import _lib
+    lib = _lib.load()
+
+    def get():
+        d, h = ctypes.c_double(0.0), ctypes.c_double(0.0)
+        lib.nlosgr_get_batch_budgets(ctypes.byref(d), ctypes.byref(h))
+        return d.value, h.value
+
+    before = get()
+    try:
+        lib.nlosgr_set_batch_budgets(77.0, 55.0)
+        with _lib.batch_budgets(drho_mb=3.0):
+            assert get() == (3.0, 55.0)
+            with _lib.batch_budgets(tile_hpart_mb=9.0):
+                assert get() == (3.0, 9.0)
+            assert get() == (3.0, 55.0)
+        assert get() == (77.0, 55.0)
+        lib.nlosgr_set_batch_budgets(-5.0, 0.0)      # <= 0 keeps the current values
+        assert get() == (77.0, 55.0)
+    finally:
+        lib.nlosgr_set_batch_budgets(*before)
