@@ -1199,7 +1199,8 @@ __global__ __launch_bounds__(kBlock) void fwd_dense_kernel(KArgs k) {
 #endif
 constexpr int kBSteps = NLOSGR_BSTEPS;   // bins per lane per backward drain round
 #ifndef NLOSGR_BSTEPS_NETF
-#define NLOSGR_BSTEPS_NETF 16
+// 20 since round 5 (spill-free with the SGPR wave index; C3 netf bwd 1684 -> 1618 ms; 24 spills 12 B)
+#define NLOSGR_BSTEPS_NETF 20
 #endif
 #ifndef NLOSGR_BPREFIX
 #define NLOSGR_BPREFIX 1   // no-occlusion culled backward: moments by nested running sums (see bwd_kernel)
