@@ -13,6 +13,10 @@
 //   mode 8: as mode 1 with every other lane active (32 active, all four 16-lane groups busy)
 //   mode 9: as mode 6 with lanes 0-31 active
 //   mode 10: ds_add_f32 (no return) at random bins, one bin per op (build with -munsafe-fp-atomics)
+//   mode 11: ds_add_u64, lane l at word base + (l mod 16) + 32 (l / 16): distinct mod 16 within each
+//            16-lane group, lanes l and l + 16 on the same word mod 32 (which lane grouping banks it?)
+//   mode 12: ds_add_u64, lane l at word base + (l mod 32) + 64 (l / 32): distinct mod 32 within each half
+//   mode 13: ds_add_u64, lane l at word base + 16 (l mod 4) + (l / 4): 16-lane groups hold 4 runs of 4
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdint.h>
@@ -28,9 +32,11 @@ constexpr int kBins = 1024, kSteps = 20, kIters = 2000, kBlocks = 256 * 12;
 template <int MODE>
 __global__ __launch_bounds__(256) void bench(float* out, int seed) {
     constexpr bool ATOM = MODE == 1 || MODE == 3 || MODE == 4 || (MODE >= 6 && MODE != 10);
+    constexpr bool PATTERN = MODE >= 11;
     constexpr int SPREAD = (MODE == 2 || MODE == 3) ? 48 : ((MODE == 4 || MODE == 5) ? 12 : 0);
     __shared__ __align__(16) unsigned h32[4 * (kBins + 192)];
     for (int t = threadIdx.x; t < 4 * (kBins + 192); t += 256) h32[t] = 0u;
+    (void)PATTERN;
     __syncthreads();
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     unsigned st = (unsigned)(lane * 2654435761u) ^ (unsigned)(seed + blockIdx.x * 7919);
@@ -39,7 +45,12 @@ __global__ __launch_bounds__(256) void bench(float* out, int seed) {
     for (int it = 0; it < kIters; ++it) {
         st = st * 1664525u + 1013904223u;
         int pos;
-        if (MODE == 6 || MODE == 9) {
+        if (PATTERN) {
+            const int b = (int)(__builtin_amdgcn_readfirstlane((st >> 8) % (kBins - 300)) & ~1);
+            const int w = MODE == 11 ? (lane % 16) + 32 * (lane / 16)
+                        : MODE == 12 ? (lane % 32) + 64 * (lane / 32) : 16 * (lane % 4) + lane / 4;
+            pos = b + 2 * (w % 128);
+        } else if (MODE == 6 || MODE == 9) {
             pos = (int)(__builtin_amdgcn_readfirstlane((st >> 8) % (kBins - 160)) & ~1) + 2 * lane;
         } else if (SPREAD) {
             const unsigned b = __builtin_amdgcn_readfirstlane((st >> 8) % (kBins - kSteps - SPREAD));
@@ -98,7 +109,7 @@ void run(float* d) {
 int main() {
     float* d;
     hipMalloc(&d, kBlocks * 256 * sizeof(float));
-    run<0>(d); run<1>(d); run<2>(d); run<3>(d); run<4>(d); run<5>(d); run<6>(d); run<7>(d); run<8>(d); run<9>(d); run<10>(d);
+    run<0>(d); run<1>(d); run<2>(d); run<3>(d); run<4>(d); run<5>(d); run<6>(d); run<7>(d); run<8>(d); run<9>(d); run<10>(d); run<11>(d); run<12>(d); run<13>(d);
     hipFree(d);
     return 0;
 }
