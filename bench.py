@@ -546,6 +546,13 @@ def main():
             out["cpu_baseline"] = cpu_baseline(a.config, a.cutoff, preset=a.preset, mode=a.mode)
         except Exception as e:  # report, never fake
             out["cpu_baseline"] = {"value": None, "error": repr(e)}
+        if a.config == "C3" and (a.preset, a.mode, a.selection) == ("cuda", "noocl", "support"):
+            # BASELINE.json configs[0] (1k Gaussians -> 32x32x128 on the CPU, the reference's torch path:
+            # torch preset, dense) timed in the same run, for the record beside the headline's baseline
+            try:
+                out["cpu_baseline_c1"] = cpu_baseline("C1", 0.0, preset="torch", mode="noocl")
+            except Exception as e:
+                out["cpu_baseline_c1"] = {"value": None, "error": repr(e)}
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -103,13 +103,13 @@ def test_adam_rejects_bad_args():
     assert b"step" in lib.nlosgr_last_error()
 
 
-def _scene_model(dev, ng=400, H=6, W=5, T=48, seed=3):
+def _scene_model(dev, ng=400, H=6, W=5, T=48, seed=3, cutoff=3.0):
     from nlosgr import GaussianParams
     from nlosgr.volume import Scene, make_config
     scene = Scene(H=H, W=W, T=T, ns=8)
     model = GaussianParams.synthetic(ng, 3, preset="cuda", device=dev, seed=seed)
     geo = scene.geometry(dev, "cuda", "noocl")
-    cfg = make_config(model, scene, "cuda", "noocl", cutoff=3.0)
+    cfg = make_config(model, scene, "cuda", "noocl", cutoff=cutoff)
     g = torch.Generator().manual_seed(seed + 1)
     target = (torch.rand(H * W, T, generator=g) * 1e-3).to(dev)
     return scene, model, geo, cfg, target
@@ -230,7 +230,7 @@ def test_bucketed_backward_equals_full():
         render_backward(*args, geo, cfg, grad_hist=grad, g_range=(100, 300))   # not a multiple of 256
 
 
-def _shard_worker(rank, world, port, out):
+def _shard_worker(rank, world, port, out, cutoff=3.0):
     import os
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -241,7 +241,7 @@ def _shard_worker(rank, world, port, out):
         from nlosgr.distributed import wall_rows
         from nlosgr.train import TrainStep
         dev = torch.device("cuda:0")
-        scene, model, geo, cfg, target = _scene_model(dev, ng=1500)
+        scene, model, geo, cfg, target = _scene_model(dev, ng=1500, cutoff=cutoff)
         idx = wall_rows(scene.H, scene.W, rank, world, device=dev)   # the split bench.py --gpus N uses
         step = TrainStep(model, geo.rows(idx), cfg, target[idx].contiguous(), gt_times=100.0, buckets=4)
         losses = [step(it).cpu() for it in range(2)]
@@ -251,10 +251,13 @@ def _shard_worker(rank, world, port, out):
         dist.destroy_process_group()
 
 
-def test_sharded_train_step_matches_single_process():
+@pytest.mark.parametrize("cutoff", [3.0, 5.7])
+def test_sharded_train_step_matches_single_process(cutoff):
     """Two gloo ranks sharing the GPU, each training its row-interleaved wall shard (wall_rows, as
     bench.py --gpus N shards; bucketed, overlapped gradient all-reduce, TrainStep.buckets = 4) ==
-    one process training the whole wall."""
+    one process training the whole wall.  At 5.7 sigma (no ray cache) both run the slab-
+    ordered forward and backward, so the bucketed exchange sums permuted gradient rows and scatters
+    them back on every rank."""
     import socket
     import torch.multiprocessing as mp
     from nlosgr.train import TrainStep
@@ -263,9 +266,9 @@ def test_sharded_train_step_matches_single_process():
     port = s.getsockname()[1]
     s.close()
     out = mp.Manager().dict()
-    mp.spawn(_shard_worker, args=(2, port, out), nprocs=2, join=True)
+    mp.spawn(_shard_worker, args=(2, port, out, cutoff), nprocs=2, join=True)
     dev = torch.device("cuda:0")
-    scene, model, geo, cfg, target = _scene_model(dev, ng=1500)
+    scene, model, geo, cfg, target = _scene_model(dev, ng=1500, cutoff=cutoff)
     step = TrainStep(model, geo, cfg, target, gt_times=100.0)
     losses = [step(it).cpu() for it in range(2)]
     for r in range(2):
@@ -276,6 +279,26 @@ def test_sharded_train_step_matches_single_process():
             # band sums add in another order: Adam's first steps ~ lr sign(g) can flip a near-zero gradient
             bad = ((a - b.detach().cpu()).abs() > 1e-5 * (1 + b.detach().cpu().abs())).float().mean().item()
             assert bad < 2e-3, (n, bad)
+
+
+def test_train_step_orders_match_given_order():
+    """at 5.7 sigma (no ray cache) TrainStep renders the forward and the backward on
+    slab-permuted Gaussians and scatters the six gradients back; its gradients and loss equal those of
+    the step in the given order up to fp32 summation order (2e-5 of each tensor's max; rotation 2e-4)."""
+    from nlosgr.train import TrainStep
+    dev = torch.device("cuda:0")
+    grads, losses = [], []
+    for order in ("slab", None):
+        scene, model, geo, cfg, target = _scene_model(dev, ng=3000, H=8, W=8, T=64, cutoff=5.7)
+        step = TrainStep(model, geo, cfg, target, gt_times=100.0, keep_grads=True, bwd_order=order, fwd_order=order)
+        assert (step.fwd_order, step.bwd_order) == (order, order)
+        losses.append(step().cpu())
+        grads.append([g.detach().cpu() for g in step.grads])
+    torch.testing.assert_close(losses[0], losses[1], rtol=2e-6, atol=0)
+    for name, a, b in zip(("mu", "f_dc", "f_rest", "opacity", "scaling", "rotation"), *grads):
+        err = float((a - b).abs().max() / b.abs().max())
+        tol = 2e-4 if name == "rotation" else 2e-5   # (the quaternion Jacobian cancels: test_gpu_fullsize)
+        assert float(b.abs().max()) > 0 and err <= tol, (name, err)
 
 
 def _rccl_worker(rank, world, port, out):
