@@ -111,6 +111,14 @@ constexpr float kAngMargin = 1e-4f;
 // the netf transmittance factor exp(-sigma pdf c dT) without an exp when c dT <= 1/64 (C3: 1.25e-3;
 // sigma <= 1, pdf <= 1), a launch-uniform choice
 constexpr float kSmallX = 1.0f / 64.0f;
+constexpr float kTf0 = 1.0f + 1e-7f;   // the netf transmittance factor's constant, exp(0) + 1e-7 in float
+constexpr float kRTf0 = 1.0f / kTf0;
+template <int N>
+__device__ __forceinline__ constexpr float kTfPow() {   // kTf0^N (exact in float for small N: 1 + N 2^-23)
+    float r = 1.0f;
+    for (int i = 0; i < N; ++i) r *= kTf0;
+    return r;
+}
 __device__ __forceinline__ float om_exp_small(float x) {
     return x * fmaf(x, fmaf(x, fmaf(x, -1.0f / 24.0f, 1.0f / 6.0f), -0.5f), 1.0f);
 }
@@ -825,15 +833,19 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
                     // + 1e-7), two bins per float2 read-add-write; slot 0 before pos (o = 1, a segment's
                     // first round) adds 0 and leaves T as it is
                     float cur = fast_exp2(fmaf(d.ga, t * t, d.al));   // seeded at pos (see above)
-                    float q = fast_exp2(d.ga * fmaf(2.f, t, 1.f));
+                    // the recurrence runs on p~_m = pdf_m c0^m and the transmittance on T~_m = T_m / c0^m (m = bins
+                    // past pos, c0 = kTf0 = 1 + 1e-7): v_m = T~_m p~_m = T_m pdf_m and T~_{m+1} = T~_m f_m / c0 =
+                    // T~_m + v_m g(p~_m) with g the cubic's p-terms over c0, one fma per bin (T rescaled per round)
+                    float q = fast_exp2(d.ga * fmaf(2.f, t, 1.f)) * kTf0;
                     const float cc = fast_exp2(2.f * d.ga);
                     // the TAIL netf forward runs only at c dT <= kSmallX, so x = sigma pdf c dT <= 1/64 and
-                    // exp(-x) + 1e-7 is the cubic the backward uses (truncation x^4 / 24 <= 2.5e-9): no exp
+                    // exp(-x) + 1e-7 is the cubic the backward uses (truncation x^4 / 24 <= 2.5e-9): no exp.
+                    // As a cubic in pdf: f = c0 + e1 pdf + e2 pdf^2 + e3 pdf^3, e1 = -sx, e2 = sx^2 / 2, e3 =
+                    // -sx^3 / 6 (the 1e-7 folded into c0: 1 + 1e-7 rounds to 1 + 2^-23, 1.9e-8 per bin); g takes
+                    // p~ for pdf, 1 + 2.4e-6 relative at most within a round: f off by <= 2.4e-6 x per bin
                     const float sx = d.sc;
-                    auto tfac = [sx](float pv) {
-                        const float x = pv * sx;
-                        return fmaf(x, fmaf(x, fmaf(x, -1.0f / 6.0f, 0.5f), -1.0f), 1.0f) + 1e-7f;
-                    };
+                    const float e1 = -sx * kRTf0, e2 = 0.5f * sx * sx * kRTf0, e3 = (-1.0f / 6.0f) * sx * sx * sx * kRTf0;
+                    auto gfac = [e1, e2, e3](float pv) { return fmaf(pv, fmaf(pv, e3, e2), e1); };
                     float2* hb2 = reinterpret_cast<float2*>(hb);
 #pragma unroll
                     for (int kv = 0; kv < kSteps / VW; ++kv) {
@@ -848,18 +860,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
                         const float p1 = cur;
                         cur *= q;
                         q *= cc;
-                        const float f0 = tfac(p0);
-                        float v0 = T * p0;   // T carries w c dT sin(theta) (set at the segment's start)
-                        if (kv == 0) {
-                            v0 = o ? 0.f : v0;
-                            T = o ? T : T * f0;
-                        } else {
-                            T *= f0;
-                        }
+                        // T carries w c dT sin(theta) (set at the segment's start); slot 0 before pos adds 0 and
+                        // (v0 = 0) leaves T as it is
+                        const float v0 = (kv == 0 && o) ? 0.f : T * p0;
+                        T = fmaf(v0, gfac(p0), T);
                         const float v1 = T * p1;
-                        T *= tfac(p1);
+                        T = fmaf(v1, gfac(p1), T);
                         emit2<FX>(hb2 + kv, v0, v1);
                     }
+                    T *= o ? kTfPow<kSteps - 1>() : kTfPow<kSteps>();   // T = T~ c0^(bins advanced)
                 } else if (win) {
                     float cur = fast_exp2(fmaf(d.ga, t * t, d.al));
                     float q = fast_exp2(d.ga * fmaf(2.f, t, 1.f));
@@ -1208,6 +1217,14 @@ constexpr int kBSteps = NLOSGR_BSTEPS;   // bins per lane per backward drain rou
 // 20 since round 5 (spill-free with the SGPR wave index; C3 netf bwd 1684 -> 1618 ms; 24 spills 12 B)
 #define NLOSGR_BSTEPS_NETF 20
 #endif
+#ifndef NLOSGR_BWD_WPE
+#define NLOSGR_BWD_WPE 4   // backward: minimum waves per SIMD (4: <= 128 VGPRs)
+#endif
+#ifndef NLOSGR_BSTEPS_NETF_TAIL
+// netf TAIL rounds (round 5: exp-free cubic in pdf, D = drho / (sigma c dT); C3 netf bwd 1500 / 1478 / 1468 /
+// 1485 ms at 24 / 28 / 32 / 36 bins; 32 spills 36 B per lane, in the wall-point loop, not in the drain)
+#define NLOSGR_BSTEPS_NETF_TAIL 32
+#endif
 #ifndef NLOSGR_BPREFIX
 #define NLOSGR_BPREFIX 1   // no-occlusion culled backward: moments by nested running sums (see bwd_kernel)
 #endif
@@ -1218,7 +1235,8 @@ constexpr int kBSteps = NLOSGR_BSTEPS;   // bins per lane per backward drain rou
 #define NLOSGR_BSTEPS_TAIL 40
 #endif
 // the staged gradient row is zero-padded by the longest round (no-occlusion TAIL rounds)
-constexpr int kBPad = NLOSGR_BSTEPS_TAIL > kBSteps ? NLOSGR_BSTEPS_TAIL : kBSteps;
+constexpr int kBPad = NLOSGR_BSTEPS_TAIL > kBSteps ? (NLOSGR_BSTEPS_TAIL > NLOSGR_BSTEPS_NETF_TAIL ? NLOSGR_BSTEPS_TAIL : NLOSGR_BSTEPS_NETF_TAIL)
+                                                    : (kBSteps > NLOSGR_BSTEPS_NETF_TAIL ? kBSteps : NLOSGR_BSTEPS_NETF_TAIL);
 constexpr int kBwdSlots = 13;   // per-Gaussian backward partial: dA[9], dMu[3], dsigma (stride 32 in HBM)
 constexpr int kShPart = 28;     // sh_kernel partial: dF[KM <= 25], dMu[3] (at KM), pad
 
@@ -1384,14 +1402,14 @@ __device__ unsigned long long g_bdbg[8];
 #endif
 
 template <int PRESET, int MODE, bool DENSE, bool RAYS, bool CACHE, bool SHR, bool TAIL = false>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) void bwd_kernel(KArgs k) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_BWD_WPE, 8))) void bwd_kernel(KArgs k) {
 #ifdef NLOSGR_BCOUNT
     unsigned long long bdbg[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #endif
     // bins per drain round: netf keeps more per-ray state, so its rounds are shorter (no spill at 128 VGPRs)
     // (the no-occlusion TAIL rounds are longer: 32 bins measured 1137 vs 1170 ms at 24 on C3, and only
     // that variant stays spill-free at 32)
-    constexpr int kRS = MODE == NLOSGR_MODE_NETF ? NLOSGR_BSTEPS_NETF
+    constexpr int kRS = MODE == NLOSGR_MODE_NETF ? (TAIL && !RAYS && !DENSE ? NLOSGR_BSTEPS_NETF_TAIL : NLOSGR_BSTEPS_NETF)
                         : (MODE == NLOSGR_MODE_NOOCL && TAIL && !RAYS && !DENSE && !CACHE && !SHR) ? NLOSGR_BSTEPS_TAIL : kBSteps;
     static_assert(kRS <= kBPad && kRS % 4 == 0, "the staged row is padded by kBPad bins; BV4 reads whole float4s");
     extern __shared__ __align__(16) float smem[];
@@ -1429,12 +1447,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
     dMu[0] = dMu[1] = dMu[2] = 0.f;
     // this lane's Gaussian: record and feature row are re-read per wall point (L1/L2 hits) rather
     // than held in registers across the split (VGPR budget)
+    // (mu too: a register copy across the wall-point loop spilled at the longer netf rounds)
     const float* feat = k.g.features + (size_t)(active ? gi : 0) * k.g.k_feat;
-    float mu[3] = {0.f, 0.f, 0.f};
-    if (active) {
-        const GaussRec rec = k.recs[gi];
-        mu[0] = rec.a.x; mu[1] = rec.a.y; mu[2] = rec.a.z;
-    }
 
     if (shr && pbeg < pend) stage_shared(k, pbeg, nr, nt, np_, grow, tth, tph);
     int it = 0;
@@ -1474,8 +1488,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
         unsigned bx = 0u;
         if (active) {
             Pair P;
-            float mu_[3];
-            load_rec(k.recs[gi], P, mu_);
+            float mu[3];
+            load_rec(k.recs[gi], P, mu);
             if (CACHE) bx = k.cbox[o];
             if (CACHE && bx != 0u) {
                 // cached pair: u0 and the forward's albedo; no SH evaluation, no footprint (the
@@ -1575,6 +1589,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
                 // BV4 (no-occlusion TAIL): the round starts at the bin at or below pos that is a multiple of
                 // 4 and reads the row as float4 (ds_read_b128: 16-lane groups over 16 bank quads conflict
                 // less per bin than 32-lane groups over 32 bank pairs, and half the instructions)
+                // (netf TAIL measured 20 ms slower with float4 reads: C3 netf bwd 1537 -> 1557 ms)
                 constexpr bool BV4 = MODE == NLOSGR_MODE_NOOCL && TAIL && !RAYS && !DENSE;
                 constexpr int BVW = BV4 ? 4 : 2;
                 const int o = BV && act ? (b.pos & (BVW - 1)) : 0;
@@ -1715,10 +1730,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
                         // a_c sum pdf (1, m, m^2) (moments about the round's first bin, like U_n above)
                         const float sx = cdt * b.sigma;
                         const float ac = ncdt / (1.0f + 1e-7f);
-                        // the prefix P_j = rho sum_{k<=j} H_k T_k x_k = rho drho_j (rho is the pair's), so part
-                        // A's weight is c rho H_j T_j - P_j a_c = crho HT + k1 drho; sum_j c1_j pdf_j (dsigma's
-                        // part A) is UA0, summed per round below
-                        const float k1 = -b.rho * ac;
+                        // exp(-x) + 1e-7 for x = sx pdf <= 1/64 as a cubic in pdf (the x^4 / 24 term, <= 2.5e-9,
+                        // is dropped; the forward's factor, kTf0 = 1 + 1e-7 in float)
+                        const float e1 = -sx, e2 = 0.5f * sx * sx, e3 = (-1.0f / 6.0f) * sx * sx * sx;
+                        // the prefix P_j = rho sum_{k<=j} H_k T_k x_k = rho sx D_j with D_j = sum_{k<=j} H_k T_k pdf_k
+                        // (this path keeps D in b.drho; rho is the pair's), so part A's weight is
+                        // c rho H_j T_j - P_j a_c = crho (HT + kk D) with kk = -a_c sigma; sum_j c1_j pdf_j
+                        // (dsigma's part A) is crho UA0, summed per round below
+                        const float kk = -ac * b.sigma;
                         // part A's moments by nested running sums (as the no-occlusion drain): UA0 = sum hA,
                         // UA1 = sum hA w, UA2 = sum hA w (w + 1) / 2 with w = kRS - m; part B's directly
                         float UA0 = 0.f, UA1 = 0.f, UA2 = 0.f, UB0 = 0.f, UB1 = 0.f, UB2 = 0.f;
@@ -1731,15 +1750,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
                             const float pdf = cur;
                             cur *= rq;
                             rq *= rcc;
-                            const float x = pdf * sx;                 // sigma pdf c dT
-                            // exp(-x) + 1e-7 for x <= 1/64 (the x^4 / 24 term, <= 2.5e-9, is dropped)
-                            const float f = fmaf(x, fmaf(x, fmaf(x, -1.0f / 6.0f, 0.5f), -1.0f), 1.0f) + 1e-7f;
+                            const float f = fmaf(pdf, fmaf(pdf, fmaf(pdf, e3, e2), e1), kTf0);
                             const float HT = Hs[m] * T;
-                            const float hdt = HT * x;
-                            drho += hdt;
-                            const float c1 = in ? fmaf(k1, drho, crho * HT) : 0.f;
+                            drho = fmaf(HT, pdf, drho);               // D
+                            const float c1 = in ? fmaf(kk, drho, HT) : 0.f;
                             const float pin = in ? pdf : 0.f;
-                            UA0 = fmaf(c1, pdf, UA0);                 // x sigma at the end
+                            UA0 = fmaf(c1, pdf, UA0);                 // x crho sigma at the end
                             UA1 += UA0;
                             UA2 += UA1;
                             UB0 += pin;
@@ -1747,11 +1763,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
                             UB2 = fmaf(pin, (float)(m * m), UB2);
                             T *= in ? f : 1.f;
                         }
-                        dsig += UA0;
-                        pre = b.rho * drho;
+                        dsig = fmaf(crho, UA0, dsig);
+                        pre = b.rho * sx * drho;
                         // S_n += sum h (kb + m)^n, kb = the round's first bin offset
                         const float kb = kseed;
-                        const float sg = b.sigma, sgb = b.sigma * ac;
+                        const float sg = b.sigma * crho, sgb = b.sigma * ac;
                         const float KA = kb + (float)kRS;   // kap at slot kRS
                         S0 = fmaf(sg, UA0, S0);
                         S1 = fmaf(sg, fmaf(KA, UA0, -UA1), S1);
@@ -1823,7 +1839,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
                             S0 *= b.w; S1 *= b.w; S2 *= b.w;
                         } else {
                             rSig = fmaf(b.pre, b.dsigb, b.dsig);
-                            rRho = b.drho;
+                            // (the exp-free culled drain keeps D = drho / (sigma c dT) in b.drho)
+                            rRho = !DENSE && (small_x || TAIL) ? b.drho * (cdt * b.sigma) : b.drho;
                         }
                         for (int r = 0; r < 3; ++r) {
                             const float zv = S0 * b.zs[r] + S1 * b.v[r];
@@ -1886,7 +1903,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
             drho_pair = s0_pair * wrs.z;
         }
         if (active && wpair > 0.f) {
-            const float q[3] = {px - mu[0], py - mu[1], pz - mu[2]};
+            const float4 ma = k.recs[gi].a;   // mu
+            const float q[3] = {px - ma.x, py - ma.y, pz - ma.z};
             const float4* d4 = reinterpret_cast<const float4*>(pdat) + lane;
             const float4 a = d4[0], c = d4[64], e = d4[128];
             const float A[9] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w, e.x};
