@@ -70,6 +70,18 @@ constexpr int kSlot = 6;               // backward pair slot: m0 m1 m2 dsigma dr
 // lengths (a pass lasts as long as its longest walk).  C3 full-support occlusion backward 12.1 -> 10.8 s;
 // not under AABB selection (3 % slower there, and the kernel is register-bound: it keeps the plain order)
 constexpr int kWalkC0 = 96, kWalkC1 = 56, kWalkC2 = 28;   // walk-length class bounds (bins)
+// backward pair walks: unrolled x4 (the row reads run ahead without register moves; C3 occl AABB bwd
+// 2289 / 2229 / 2155 / 2146 ms at x1 / 2 / 4 / 8, x8 spills), and (NLOSGR_WALK_REC) sigma folded out of the
+// loop with 1 - exp(-x) as a quartic in pdf (2532 -> 2291 ms).  The exp2 recurrence re-seeded every kWalkR
+// steps (NLOSGR_WALK_REC=2) measured slower (2621 ms): its per-step scalar re-seed branch costs more than
+// the exp2 it saves
+#ifndef NLOSGR_WALK_UNROLL
+#define NLOSGR_WALK_UNROLL 4
+#endif
+#ifndef NLOSGR_WALK_REC
+#define NLOSGR_WALK_REC 1
+#endif
+constexpr int kWalkR = 32;             // (NLOSGR_WALK_REC=2) re-seed period
 
 struct TArgs {
     nlosgr_gaussians g;
@@ -244,6 +256,10 @@ __global__ __launch_bounds__(tile_threads<BWD>()) void tile_kernel(TArgs k) {
     const float cdt = k.opt.c_deltaT;
     const float ncdt = -cdt * kLog2e;   // exp(-x c dT) = exp2(x ncdt)
     const bool small_x = cdt <= kSmallX;  // 1 - exp(-sigma pdf c dT) by om_exp_small
+    // backward pair walks with sigma folded out and the quartic 1 - exp(-x) (kernel-uniform): walks bounded by a
+    // cutoff <= 6 sigma (for the recurrence variant: the ratio exp2(ga (2t + 1)) stays below 2^47 inside the
+    // support), and with occlusion only at c dT <= 1/64
+    const bool walk_rec = NLOSGR_WALK_REC && !DENSE && k.opt.cutoff > 0.f && mc2 <= 36.f && (!OCCL || small_x);
     const int nch = (nr + 63) / 64;
     const int deg = k.g.sh_degree, K = (deg + 1) * (deg + 1);
 
@@ -690,6 +706,57 @@ __global__ __launch_bounds__(tile_threads<BWD>()) void tile_kernel(TArgs k) {
                                 // the rows are read-only here: reads run two bins ahead of their use (past the
                                 // segment end they stay inside the LDS allocation and are not used)
                                 float2 ab0 = row[kl], ab1 = row[kl + 1];
+                                if (walk_rec) {
+                                    // sigma folded out of the loop (G = dc pdf, ps = sum dc pdf = m0 before the sigma
+                                    // scaling); occlusion at c dT <= 1/64: 1 - exp(-x), x = sigma c dT pdf, as a
+                                    // quartic in pdf.  (NLOSGR_WALK_REC=2: pdf by the exp2 recurrence, re-seeded every
+                                    // kWalkR steps; the lanes walk in lockstep, so the step count is wave-uniform)
+                                    const float kx = wsg * cdt;
+                                    const float e1 = kx, e2 = -0.5f * kx * kx, e3 = kx * kx * kx * (1.0f / 6.0f),
+                                                e4 = kx * kx * kx * kx * (-1.0f / 24.0f);
+#if NLOSGR_WALK_REC == 2
+                                    const float cc = fast_exp2(2.f * ga);
+                                    float cur = 0.f, q = 0.f;
+                                    int step = 0;
+#endif
+#pragma unroll NLOSGR_WALK_UNROLL
+                                    for (int kb = kl; kb <= kh; ++kb, tt += 1.f) {
+#if NLOSGR_WALK_REC == 2
+                                        if ((__builtin_amdgcn_readfirstlane(step++) & (kWalkR - 1)) == 0) {
+                                            cur = fast_exp2(fmaf(ga, tt * tt, al));
+                                            q = fast_exp2(ga * fmaf(2.f, tt, 1.f));
+                                        }
+                                        const float pdf = cur;
+                                        cur *= q;
+                                        q *= cc;
+#else
+                                        const float pdf = fast_exp2(fmaf(ga, tt * tt, al));
+#endif
+                                        const float2 ab = ab0;
+                                        ab0 = ab1;
+                                        ab1 = row[kb + 2];
+                                        float dc;
+                                        if (OCCL) {
+                                            const float om = pdf * fmaf(pdf, fmaf(pdf, fmaf(pdf, e4, e3), e2), e1);
+                                            const float u = ab.x * rc;
+                                            dc = fmaf(-u, om, u + ab.y);   // a rho c dT (1 - om) + b
+                                            pr = fmaf(ab.x, om, pr);
+                                        } else {
+                                            dc = ab.x * wrho;
+                                            pr = fmaf(ab.x, pdf, pr);      // x sigma below
+                                        }
+                                        const float G = dc * pdf;
+                                        m0 += G;
+                                        m1 = fmaf(G, tt, m1);
+                                        m2 = fmaf(G * tt, tt, m2);
+                                    }
+                                    ps = m0;
+                                    m0 *= wsg;
+                                    m1 *= wsg;
+                                    m2 *= wsg;
+                                    if (!OCCL) pr *= wsg;
+                                } else
+#pragma unroll NLOSGR_WALK_UNROLL
                                 for (int kb = kl; kb <= kh; ++kb, tt += 1.f) {
                                     const float pdf = fast_exp2(fmaf(ga, tt * tt, al));
                                     const float cv = wsg * pdf;

@@ -225,11 +225,13 @@ def test_occl_row_cache_backward_equals_recompute(selection, cutoff):
         assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("selection,cutoff", [("support", 5.7), ("support", 0.0), ("aabb", 0.0)])
+@pytest.mark.parametrize("selection,cutoff", [("support", 5.7), ("support", 3.0), ("support", 0.0), ("aabb", 5.7),
+                                              ("aabb", 0.0)])
 def test_occl_small_cdt_polynomial(selection, cutoff):
     """c dT <= 1/64 (C3: 1.25e-3) takes the polynomial 1 - exp(-x) = x (1 - x/2 + x^2/6 - x^3/24)
     (x = sigma pdf c dT <= c dT) in the forward rows and the backward pairs pass: same oracle
-    comparison as above at c dT = 0.015."""
+    comparison as above at c dT = 0.015.  At cutoffs in (0, 6] the backward walks take pdf from the exp2
+    recurrence and 1 - exp(-x) as a quartic in pdf (the C3 occlusion lines' path)."""
     from nlosgr.render import bboxes
     walls, box = _scene()
     m = _model(70, 2, 31, 1.2, 3.0)
