@@ -35,6 +35,7 @@
 //           slot's private accumulator row (plain read-modify-write).
 //   finish: sums each Gaussian's slot rows in slot order and chains to the raw parameters.
 #include <hip/hip_runtime.h>
+#include <type_traits>
 #include <math.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -70,18 +71,19 @@ constexpr int kSlot = 6;               // backward pair slot: m0 m1 m2 dsigma dr
 // lengths (a pass lasts as long as its longest walk).  C3 full-support occlusion backward 12.1 -> 10.8 s;
 // not under AABB selection (3 % slower there, and the kernel is register-bound: it keeps the plain order)
 constexpr int kWalkC0 = 96, kWalkC1 = 56, kWalkC2 = 28;   // walk-length class bounds (bins)
-// backward pair walks: unrolled x4 (the row reads run ahead without register moves; C3 occl AABB bwd
-// 2289 / 2229 / 2155 / 2146 ms at x1 / 2 / 4 / 8, x8 spills), and (NLOSGR_WALK_REC) sigma folded out of the
-// loop with 1 - exp(-x) as a quartic in pdf (2532 -> 2291 ms).  The exp2 recurrence re-seeded every kWalkR
-// steps (NLOSGR_WALK_REC=2) measured slower (2621 ms): its per-step scalar re-seed branch costs more than
-// the exp2 it saves
+// backward pair walks (round 5; C3 occl AABB backward, one process per build on one box): sigma folded out of
+// the loop with 1 - exp(-x) as a quartic in pdf 2532 -> 2291 ms (a diagnostic build with the polynomial cut
+// to one multiply: -9 %, without the row reads: -2.6 %: the walks are VALU-bound), unrolled x4 (the row reads
+// run ahead without register moves; x1 / 2 / 4 / 8: 2289 / 2229 / 2155 / 2146 ms, x8 spills) -> 2155, cubic
+// instead of quartic -> 2123.  Measured and dropped: the exp2 recurrence re-seeded every 32 steps (a scalar
+// branch per step: 2621 ms), or in 4-bin blocks (2131 ms), and forward rows without the per-bin support
+// mask at cutoffs >= 5 (fwd 1283 vs 1260 ms masked)
 #ifndef NLOSGR_WALK_UNROLL
 #define NLOSGR_WALK_UNROLL 4
 #endif
 #ifndef NLOSGR_WALK_REC
 #define NLOSGR_WALK_REC 1
 #endif
-constexpr int kWalkR = 32;             // (NLOSGR_WALK_REC=2) re-seed period
 
 struct TArgs {
     nlosgr_gaussians g;
@@ -526,24 +528,31 @@ __global__ __launch_bounds__(tile_threads<BWD>()) void tile_kernel(TArgs k) {
                                         const int kb = c * 64 + lane;
                                         const float kf = (float)kb;
                                         float accD = 0.f, accW = 0.f;
-                                        while (cm) {
-                                            const int s = __builtin_ctzll(cm);
-                                            cm &= cm - 1;
-                                            const int idx = __popcll(pm & ((1ull << s) - 1ull));
-                                            const float4 e0 = el[2 * idx], e1 = el[2 * idx + 1];
-                                            const int skl = __float_as_int(e1.y), slen = __float_as_int(e1.z);   // kh - kl
-                                            const float tt = kf - e0.x;
-                                            const float pdf = fast_exp2(fmaf(e0.y, tt * tt, e0.z));
-                                            // kl <= kb <= kh as one unsigned range compare
-                                            const float cv = (unsigned)(kb - skl) <= (unsigned)slen ? e0.w * pdf : 0.f;
-                                            if (OCCL) {
-                                                accD += cv;
-                                                const float w = small_x ? om_exp_small(cv * cdt) : 1.0f - fast_exp2(cv * ncdt);
-                                                accW = fmaf(e1.x, w, accW);
-                                            } else {
-                                                accW = fmaf(e1.x, cv, accW);
+                                        // the entry loop per small-c dT form (a kernel-uniform flag: one scalar branch per
+                                        // chunk instead of both forms per entry; C3 occl AABB forward 1341 -> 1260 ms)
+                                        auto entries = [&](auto smallc) {
+                                            constexpr bool kSmall = decltype(smallc)::value;
+                                            while (cm) {
+                                                const int s = __builtin_ctzll(cm);
+                                                cm &= cm - 1;
+                                                const int idx = __popcll(pm & ((1ull << s) - 1ull));
+                                                const float4 e0 = el[2 * idx], e1 = el[2 * idx + 1];
+                                                const int skl = __float_as_int(e1.y), slen = __float_as_int(e1.z);   // kh - kl
+                                                const float tt = kf - e0.x;
+                                                const float pdf = fast_exp2(fmaf(e0.y, tt * tt, e0.z));
+                                                // kl <= kb <= kh as one unsigned range compare
+                                                const float cv = (unsigned)(kb - skl) <= (unsigned)slen ? e0.w * pdf : 0.f;
+                                                if (OCCL) {
+                                                    accD += cv;
+                                                    const float w = kSmall ? om_exp_small(cv * cdt) : 1.0f - fast_exp2(cv * ncdt);
+                                                    accW = fmaf(e1.x, w, accW);
+                                                } else {
+                                                    accW = fmaf(e1.x, cv, accW);
+                                                }
                                             }
-                                        }
+                                        };
+                                        if (small_x) entries(std::integral_constant<bool, true>{});
+                                        else entries(std::integral_constant<bool, false>{});
                                         if (kb < nr) {
                                             float2 v = rows[r * nr + kb];
                                             v.x += accD;
@@ -709,35 +718,15 @@ __global__ __launch_bounds__(tile_threads<BWD>()) void tile_kernel(TArgs k) {
                                 if (walk_rec) {
                                     // sigma folded out of the loop (G = dc pdf, ps = sum dc pdf = m0 before the sigma
                                     // scaling); occlusion at c dT <= 1/64: 1 - exp(-x), x = sigma c dT pdf, as a
-                                    // quartic in pdf.  (NLOSGR_WALK_REC=2: pdf by the exp2 recurrence, re-seeded every
-                                    // kWalkR steps; the lanes walk in lockstep, so the step count is wave-uniform)
+                                    // cubic in pdf
                                     const float kx = wsg * cdt;
-                                    const float e1 = kx, e2 = -0.5f * kx * kx, e3 = kx * kx * kx * (1.0f / 6.0f),
-                                                e4 = kx * kx * kx * kx * (-1.0f / 24.0f);
-#if NLOSGR_WALK_REC == 2
-                                    const float cc = fast_exp2(2.f * ga);
-                                    float cur = 0.f, q = 0.f;
-                                    int step = 0;
-#endif
-#pragma unroll NLOSGR_WALK_UNROLL
-                                    for (int kb = kl; kb <= kh; ++kb, tt += 1.f) {
-#if NLOSGR_WALK_REC == 2
-                                        if ((__builtin_amdgcn_readfirstlane(step++) & (kWalkR - 1)) == 0) {
-                                            cur = fast_exp2(fmaf(ga, tt * tt, al));
-                                            q = fast_exp2(ga * fmaf(2.f, tt, 1.f));
-                                        }
-                                        const float pdf = cur;
-                                        cur *= q;
-                                        q *= cc;
-#else
-                                        const float pdf = fast_exp2(fmaf(ga, tt * tt, al));
-#endif
-                                        const float2 ab = ab0;
-                                        ab0 = ab1;
-                                        ab1 = row[kb + 2];
+                                    // cubic: the x^4 / 24 term is <= x^3 / 24 <= 1.6e-7 relative at x = 1/64 (C3: 8e-11)
+                                    const float e1 = kx, e2 = -0.5f * kx * kx, e3 = kx * kx * kx * (1.0f / 6.0f);
+                                    auto omf = [e1, e2, e3](float pv) { return pv * fmaf(pv, fmaf(pv, e3, e2), e1); };
+                                    auto bin = [&](float pdf, float2 ab, float t) {
                                         float dc;
                                         if (OCCL) {
-                                            const float om = pdf * fmaf(pdf, fmaf(pdf, fmaf(pdf, e4, e3), e2), e1);
+                                            const float om = omf(pdf);
                                             const float u = ab.x * rc;
                                             dc = fmaf(-u, om, u + ab.y);   // a rho c dT (1 - om) + b
                                             pr = fmaf(ab.x, om, pr);
@@ -747,8 +736,16 @@ __global__ __launch_bounds__(tile_threads<BWD>()) void tile_kernel(TArgs k) {
                                         }
                                         const float G = dc * pdf;
                                         m0 += G;
-                                        m1 = fmaf(G, tt, m1);
-                                        m2 = fmaf(G * tt, tt, m2);
+                                        m1 = fmaf(G, t, m1);
+                                        m2 = fmaf(G * t, t, m2);
+                                    };
+#pragma unroll NLOSGR_WALK_UNROLL
+                                    for (int kb = kl; kb <= kh; ++kb, tt += 1.f) {
+                                        const float pdf = fast_exp2(fmaf(ga, tt * tt, al));
+                                        const float2 ab = ab0;
+                                        ab0 = ab1;
+                                        ab1 = row[kb + 2];
+                                        bin(pdf, ab, tt);
                                     }
                                     ps = m0;
                                     m0 *= wsg;
