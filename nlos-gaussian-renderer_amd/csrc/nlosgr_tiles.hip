@@ -77,7 +77,8 @@ constexpr int kWalkC0 = 96, kWalkC1 = 56, kWalkC2 = 28;   // walk-length class b
 // run ahead without register moves; x1 / 2 / 4 / 8: 2289 / 2229 / 2155 / 2146 ms, x8 spills) -> 2155, cubic
 // instead of quartic -> 2123.  Measured and dropped: the exp2 recurrence re-seeded every 32 steps (a scalar
 // branch per step: 2621 ms), or in 4-bin blocks (2131 ms), and forward rows without the per-bin support
-// mask at cutoffs >= 5 (fwd 1283 vs 1260 ms masked)
+// mask at cutoffs >= 5 (fwd 1283 vs 1260 ms masked), and two entries per forward loop iteration with both records
+// read first (fwd 1335 vs 1260 ms; full support 6974 vs 6217)
 #ifndef NLOSGR_WALK_UNROLL
 #define NLOSGR_WALK_UNROLL 4
 #endif
