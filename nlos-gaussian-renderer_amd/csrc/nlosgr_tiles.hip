@@ -78,7 +78,11 @@ constexpr int kWalkC0 = 96, kWalkC1 = 56, kWalkC2 = 28;   // walk-length class b
 // instead of quartic -> 2123.  Measured and dropped: the exp2 recurrence re-seeded every 32 steps (a scalar
 // branch per step: 2621 ms), or in 4-bin blocks (2131 ms), and forward rows without the per-bin support
 // mask at cutoffs >= 5 (fwd 1283 vs 1260 ms masked), and two entries per forward loop iteration with both records
-// read first (fwd 1335 vs 1260 ms; full support 6974 vs 6217)
+// read first (fwd 1335 vs 1260 ms; full support 6974 vs 6217), and a cubic 1 - exp(-x) in the forward rows
+// (1268 vs 1265 ms: no gain)
+#ifndef NLOSGR_TILE_OM3
+#define NLOSGR_TILE_OM3 1
+#endif
 #ifndef NLOSGR_WALK_UNROLL
 #define NLOSGR_WALK_UNROLL 4
 #endif
@@ -545,7 +549,14 @@ __global__ __launch_bounds__(tile_threads<BWD>()) void tile_kernel(TArgs k) {
                                                 const float cv = (unsigned)(kb - skl) <= (unsigned)slen ? e0.w * pdf : 0.f;
                                                 if (OCCL) {
                                                     accD += cv;
-                                                    const float w = kSmall ? om_exp_small(cv * cdt) : 1.0f - fast_exp2(cv * ncdt);
+                                                    // (small x: the cubic x (1 - x/2 + x^2/6), x^4/24 <= 1.6e-7 relative at 1/64)
+                                                    float w;
+                                                    if (kSmall) {
+                                                        const float x = cv * cdt;
+                                                        w = NLOSGR_TILE_OM3 ? x * fmaf(x, fmaf(x, 1.0f / 6.0f, -0.5f), 1.0f) : om_exp_small(x);
+                                                    } else {
+                                                        w = 1.0f - fast_exp2(cv * ncdt);
+                                                    }
                                                     accW = fmaf(e1.x, w, accW);
                                                 } else {
                                                     accW = fmaf(e1.x, cv, accW);
