@@ -64,7 +64,13 @@ constexpr float kFullM2 = 180.0f;      // AABB selection: whole-ray support, pdf
 constexpr float kLog2e = 1.44269504088896341f;
 constexpr int kRowFloats = 32768;      // [ray][bin] float2 rows: 128 KB
 constexpr int kList = 20;              // live entries per wave list pass (8 floats each)
-constexpr int kCullU = 2;              // cull: Gaussians per thread per round (one barrier pair per kCullU x threads)
+#ifndef NLOSGR_CULL_U_BWD
+#define NLOSGR_CULL_U_BWD 4
+#endif
+// cull: Gaussians per thread per round (one barrier pair per kCullU x threads); the forward's LDS holds 2
+// (rows + stage + queue + lists: 157.5 of 160 KB), the backward's 8 waves leave room for 4
+template <bool BWD>
+constexpr int cull_u() { return BWD ? NLOSGR_CULL_U_BWD : 2; }
 constexpr int kSlot = 6;               // backward pair slot: m0 m1 m2 dsigma drho | key
 // support selection, backward: a block's live (entry, ray) pairs are walked in passes of 64 sorted by
 // walk-length class (longest first) when there is more than one pass, so a pass's lanes walk similar
@@ -127,7 +133,7 @@ struct TLayout {   // offsets in floats
         rows = 0;
         stage = rows + 2 * rt * nr;
         queue = stage + kWin * kStage;
-        misc = queue + kCullU * tb + kWin;   // queue capacity: one cull round + one window
+        misc = queue + (bwd ? cull_u<true>() : cull_u<false>()) * tb + kWin;   // queue: one cull round + one window
         comb = misc + 256;
         // shared scratch: backward combine [kWin][16] / (rays phase) per-wave entry lists
         // [waves][kList][8] / (backward pairs) per-wave pair slots [waves][64][kSlot]
@@ -249,7 +255,8 @@ __global__ __launch_bounds__(tile_threads<BWD>()) void tile_kernel(TArgs k) {
     float* misc = sm + L.misc;
     int* icnt = reinterpret_cast<int*>(misc);          // [64] AABB cap counters per ray
     int* ihalf = icnt + 64;                             // [64] per-window hits of the first staged half
-    int* iwave = icnt + 128;                            // [kCullU][16] cull counts per wave
+    constexpr int kCullU = cull_u<BWD>();
+    int* iwave = icnt + 128;                            // [kCullU][16] cull counts per wave (<= 64 ints)
     float* cone = misc + 160;                           // axis xyz, cos h, sin h, pass-all flag
     const int tid = threadIdx.x, wave = tid >> 6, lane = lane_id();
     const int RT = k.rt;
