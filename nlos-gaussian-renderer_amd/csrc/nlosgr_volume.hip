@@ -1220,6 +1220,11 @@ constexpr int kBSteps = NLOSGR_BSTEPS;   // bins per lane per backward drain rou
 #ifndef NLOSGR_BWD_WPE
 #define NLOSGR_BWD_WPE 4   // backward: minimum waves per SIMD (4: <= 128 VGPRs)
 #endif
+#ifndef NLOSGR_BSTEPS_TAIL_SHR
+// the shared-row layout's TAIL rounds (C5: bwd 941 / 855 / 824 ms per shard at 24 / 32 / 40 bins; 40 spills
+// 64 B per lane in the wall-point loop, none in the drain)
+#define NLOSGR_BSTEPS_TAIL_SHR 40
+#endif
 #ifndef NLOSGR_BSTEPS_NETF_TAIL
 // netf TAIL rounds (round 5: exp-free cubic in pdf, D = drho / (sigma c dT); C3 netf bwd 1500 / 1478 / 1468 /
 // 1485 ms at 24 / 28 / 32 / 36 bins; 32 spills 36 B per lane, in the wall-point loop, not in the drain)
@@ -1235,8 +1240,8 @@ constexpr int kBSteps = NLOSGR_BSTEPS;   // bins per lane per backward drain rou
 #define NLOSGR_BSTEPS_TAIL 40
 #endif
 // the staged gradient row is zero-padded by the longest round (no-occlusion TAIL rounds)
-constexpr int kBPad = NLOSGR_BSTEPS_TAIL > kBSteps ? (NLOSGR_BSTEPS_TAIL > NLOSGR_BSTEPS_NETF_TAIL ? NLOSGR_BSTEPS_TAIL : NLOSGR_BSTEPS_NETF_TAIL)
-                                                    : (kBSteps > NLOSGR_BSTEPS_NETF_TAIL ? kBSteps : NLOSGR_BSTEPS_NETF_TAIL);
+constexpr int kmax_i(int a, int b) { return a > b ? a : b; }
+constexpr int kBPad = kmax_i(kmax_i(NLOSGR_BSTEPS_TAIL, kBSteps), kmax_i(NLOSGR_BSTEPS_NETF_TAIL, NLOSGR_BSTEPS_TAIL_SHR));
 constexpr int kBwdSlots = 13;   // per-Gaussian backward partial: dA[9], dMu[3], dsigma (stride 32 in HBM)
 constexpr int kShPart = 28;     // sh_kernel partial: dF[KM <= 25], dMu[3] (at KM), pad
 
@@ -1410,7 +1415,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_B
     // (the no-occlusion TAIL rounds are longer: 32 bins measured 1137 vs 1170 ms at 24 on C3, and only
     // that variant stays spill-free at 32)
     constexpr int kRS = MODE == NLOSGR_MODE_NETF ? (TAIL && !RAYS && !DENSE ? NLOSGR_BSTEPS_NETF_TAIL : NLOSGR_BSTEPS_NETF)
-                        : (MODE == NLOSGR_MODE_NOOCL && TAIL && !RAYS && !DENSE && !CACHE && !SHR) ? NLOSGR_BSTEPS_TAIL : kBSteps;
+                        : (MODE == NLOSGR_MODE_NOOCL && TAIL && !RAYS && !DENSE && !CACHE && !SHR) ? NLOSGR_BSTEPS_TAIL
+                        : (MODE == NLOSGR_MODE_NOOCL && TAIL && !RAYS && !DENSE && !CACHE && SHR) ? NLOSGR_BSTEPS_TAIL_SHR : kBSteps;
     static_assert(kRS <= kBPad && kRS % 4 == 0, "the staged row is padded by kBPad bins; BV4 reads whole float4s");
     extern __shared__ __align__(16) float smem[];
     const int nr = k.geo.nr, nt = k.geo.nt, np_ = k.geo.np;
