@@ -1236,7 +1236,8 @@ constexpr int kBSteps = NLOSGR_BSTEPS;   // bins per lane per backward drain rou
 #ifndef NLOSGR_BSTEPS_TAIL
 // (round 4's 40-bin rounds spilled 36 B per lane, reloaded and re-stored every wall point: ~1.2 GB of
 // scratch writes per launch reached HBM.  The wave index read as an SGPR (readfirstlane) keeps the
-// wave-derived LDS bases out of VGPRs and the kernel spill-free at 40; 32 bins cost ~30 ms per step)
+// wave-derived LDS bases out of VGPRs and the kernel spill-free at 40; 32 bins cost ~30 ms per step;
+// 48 / 56 bins: 767 / 776 vs 773 ms with 16 / 44 B of spills per lane — kept at 40, spill-free)
 #define NLOSGR_BSTEPS_TAIL 40
 #endif
 // the staged gradient row is zero-padded by the longest round (no-occlusion TAIL rounds)
