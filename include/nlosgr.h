@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define NLOSGR_ABI_VERSION 7
+#define NLOSGR_ABI_VERSION 8
 
 /* convention presets */
 enum {
@@ -112,7 +112,10 @@ typedef struct {
     float c_deltaT;           /* c * deltaT (netf transmittance) */
     float ray_scale;          /* scale applied to the optional per-ray output (e.g. c*dT) */
     int32_t nsplit;           /* backward: wall-point splits (0 -> auto) */
-    int32_t flags;            /* diagnostics only (phase ablation), 0 */
+    int32_t flags;            /* 0 in production.  Bits 0-6: phase-ablation diagnostics (wrong results on
+                                 purpose); NLOSGR_FLAG_* below: variant selection for A/B timing and parity
+                                 cross-checks (ABI 8: these used to be environment variables, so the
+                                 library's numerics no longer depend on the caller's environment) */
     int32_t ray_cache;        /* 1: the forward records, per (wall point, Gaussian) pair, which rays
                                  of its candidate box are in support (20 B per pair in the workspace,
                                  see nlosgr_workspace_bytes) and a backward on the SAME workspace with
@@ -130,6 +133,18 @@ typedef struct {
                                  bucket while the next one is differentiated; g_end = 0 -> all */
 } nlosgr_options;
 
+/* nlosgr_options.flags: variant selection (each variant is a correct renderer of the same quantity;
+ * they differ in summation order / rounding and speed) */
+#define NLOSGR_FLAG_FLOAT_DRAIN  0x100  /* forward: fp32 claim drain instead of the fixed-point (FX) drain */
+#define NLOSGR_FLAG_MASKED_FWD   0x200  /* forward: masked (end-of-segment) drains at every cutoff, no TAIL */
+#define NLOSGR_FLAG_MASKED_BWD   0x400  /* backward: masked drains at every cutoff, no TAIL */
+#define NLOSGR_FLAG_LANE_DENSE   0x800  /* dense no-occlusion histogram through the lane-serial drain
+                                           instead of the register (lane = bin) kernel */
+#define NLOSGR_FLAG_BWD_SHARED   0x1000 /* backward: shared-row layout (4 waves per staged row) */
+#define NLOSGR_FLAG_BWD_PERWAVE  0x2000 /* backward: per-wave row layout (default picks by LDS size) */
+#define NLOSGR_FLAG_FX_MAXUNIT   0x4000 /* forward FX drain: unit from the largest amplitude bound (the round-5
+                                           rule, diagnostics: shows the precision the quantile unit recovers) */
+
 /* Scratch bytes needed by fwd/bwd for this problem (caller allocates, 256-B aligned); includes
  * nwall*ng*24 B for the ray cache when opt->ray_cache is set (OCCL mode: the row cache,
  * nwall * tiles * tile rays * nr * 8 B). */
@@ -137,8 +152,8 @@ NLOSGR_API size_t nlosgr_workspace_bytes(const nlosgr_gaussians* g, const nlosgr
                               const nlosgr_options* opt);
 
 /* Batch budgets in MiB (values <= 0 keep the current one): the backward's dL/drho buffer, filled in
- * wall-point batches (default 1024 or NLOSGR_DRHO_MB), and the ray-tile forward's partial histograms
- * (default 1024 or NLOSGR_TILE_HPART_MB); both environment variables are read once, at first use.
+ * wall-point batches (default 1024), and the ray-tile forward's partial histograms (default 1024).
+ * (ABI 8: no environment variables are read.)
  * They set the workspace layout: change them only while no workspace sized under the old values is
  * still in use (a ray-cache backward must run under the forward's budgets). */
 NLOSGR_API void nlosgr_set_batch_budgets(double drho_mb, double tile_hpart_mb);
@@ -168,6 +183,14 @@ NLOSGR_API int nlosgr_render_bwd(const nlosgr_gaussians* g, const nlosgr_geometr
 NLOSGR_API int nlosgr_count_support(const nlosgr_gaussians* g, const nlosgr_geometry* geo,
                          const nlosgr_options* opt, void* workspace, unsigned long long* counts,
                          void* hip_stream);
+
+/* Fixed-point forward state after an nlosgr_render_fwd on `workspace` (same g / geo / opt): info_out
+ * (DEVICE, [4] int32, overwritten, copied on the stream) = {E: the unit 2^-E of the fixed-point drain,
+ * E of the launch's largest amplitude bound, LDS histogram flushes into the u64 row, bright segments
+ * (peak >= 2^24 units, added straight into the u64 row)}; all zero when the forward did not take the
+ * fixed-point drain.  Diagnostics / tests. */
+NLOSGR_API int nlosgr_fx_info(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_options* opt,
+                   const void* workspace, int32_t* info_out, void* hip_stream);
 
 /* 3-sigma (sigma_scale) axis-aligned boxes [ng,6] = (min xyz, max xyz) under the preset's scale
  * convention (bbox_compute.cuh:23-71 for "cuda"; gaussian_model.py:140-178 for "torch"). */

@@ -58,21 +58,15 @@ __device__ __forceinline__ float flog2(float x) { return __builtin_amdgcn_logf(x
 inline size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
 
 // Batch budgets that shape the workspace layout (MiB): the backward's dL/drho wall-point batches and
-// the ray-tile forward's partial histograms.  Defaults come from NLOSGR_DRHO_MB / NLOSGR_TILE_HPART_MB
-// read ONCE (first use); later changes go through nlosgr_set_batch_budgets only, so a workspace sized
+// the ray-tile forward's partial histograms.  Defaults 1024 MiB each; changes go through
+// nlosgr_set_batch_budgets only (ABI 8: no environment variables, so the batch boundaries, and with
+// them the gradients' summation order, never depend on the caller's environment), so a workspace sized
 // by nlosgr_workspace_bytes and a ray-cache backward see the layout of the forward that filled it.
 struct BatchBudgets {
-    double drho_mb, tile_hpart_mb;
+    double drho_mb = 1024.0, tile_hpart_mb = 1024.0;
 };
 inline BatchBudgets& batch_budgets() {
-    static BatchBudgets b = [] {
-        BatchBudgets v;
-        const char* d = getenv("NLOSGR_DRHO_MB");
-        const char* h = getenv("NLOSGR_TILE_HPART_MB");
-        v.drho_mb = (d && atof(d) > 0.0) ? atof(d) : 1024.0;
-        v.tile_hpart_mb = (h && atof(h) > 0.0) ? atof(h) : 1024.0;
-        return v;
-    }();
+    static BatchBudgets b;
     return b;
 }
 

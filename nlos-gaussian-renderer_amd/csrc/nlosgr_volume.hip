@@ -77,7 +77,8 @@ struct KArgs {
                                  // are indexed p - pb0, so the dL/drho buffer holds one batch, not the wall)
     int accum;                   // backward batches after the first add into the partial slabs
     unsigned long long* hfx;     // forward FX drain: fixed-point histogram [P][nr] (u64, integer adds)
-    const unsigned* fx_amax;     // forward FX drain: bits of the launch's amplitude bound (fx_amax_kernel)
+    int* fx_info;                // forward FX drain: [0] unit exponent E (fx_unit_kernel), [1] E of the launch's
+                                 // largest bound, [2] LDS flushes, [3] bright segments (see kFxBits)
 };
 
 // ray cache: a pair whose (theta, phi) candidate box has at most 128 cells records which cells
@@ -468,26 +469,31 @@ constexpr float kBetaSeries = 0.5f;   // bin-integrated TAIL drain: series bin a
 // holds each bin as an unsigned 32-bit count of units 2^-E; a round adds two bins per lane with ONE
 // no-return ds_add_u64 of the packed pair (low word = even bin, high word = odd bin), so no claim table:
 // every active lane drains every round, and integer adds make the sum independent of the order (the
-// forward is bitwise deterministic whatever the schedule).  E is set per launch so that the launch's
-// amplitude bound (max over Gaussians of sigma * rho_max, fx_amax_kernel) is < 2^kFxBits units; a
-// value rounds to the nearest unit (v_cvt_rpi_i32_f32), i.e. the absolute error per term is <= 2^-(kFxBits+1)
-// of the brightest possible term.  A low word must never carry into its high word: every lane sums the
-// peaks (exp2 of the segment's log2 amplitude, in units) of the segments it took since the last check;
-// a segment adds at most its peak to any bin once, so while every lane's sum stays <= thr the largest
-// field stays <= M + 64 thr < 2^32.  When a lane passes thr the wave reads its histogram's true maximum
-// M; past 2^31 it moves the fields into the u64 histogram in global memory (integer atomics; rare) and
-// zeroes them.  At the end each workgroup adds its 4 waves' fields to the global u64 histogram [P][nr]
-// (all Gaussian splits of a wall point meet there), and fx_reduce_kernel scales it to floats.
+// forward is bitwise deterministic whatever the schedule).  A value rounds to the nearest unit
+// (v_cvt_rpi_i32_f32).
+// The unit (round 6): E is set per launch from the amplitude bounds b_g = sigma_g * rho_max_g of the
+// Gaussians (fx_bound_kernel; rho_max by Cauchy-Schwarz on the SH bands) so that the bound of the
+// ceil(ng/256)-th brightest Gaussian is < 2^kFxBits units (fx_unit_kernel, a quantile over the bounds'
+// binary exponents), not the largest bound: a few very bright Gaussians no longer coarsen the unit of
+// all the others (round 5 used the maximum, so 0.1 % of Gaussians 10^3-10^4 x brighter than the rest cost
+// the rest 10-13 bits, and their sub-half-unit tails rounded to zero: a one-sided bias).  A segment whose
+// peak is >= 2^kFxBits units at refill ("bright"; at most the segments of the ceil(ng/256) Gaussians above
+// the quantile, and none unless the bounds spread by more than the C-S slack) bypasses the LDS: its lane
+// adds its values as u64 integers straight into the wall point's global u64 row (agent-scope atomics), so
+// it is as exact as the rest.  E is clamped to <= E(max bound) + kFxRange so those u64 sums cannot wrap.
+// A low word must never carry into its high word: every lane sums the peaks (exp2 of the segment's log2
+// amplitude, in units) of the LDS segments it took since the last check; a segment adds at most its peak
+// to any bin once, so while every lane's sum stays <= thr the largest field stays <= M + 64 thr < 2^32.
+// When a lane passes thr the wave reads its histogram's true maximum M; past 2^31 it moves the fields into
+// the u64 row in global memory (integer atomics) and zeroes them.  At the end each workgroup adds its 4
+// waves' fields to the global u64 histogram [P][nr] (all Gaussian splits of a wall point meet there), and
+// fx_reduce_kernel scales it to floats.
 constexpr int kFxBits = 24;
+constexpr int kFxRange = 20;                 // E <= E(max bound) + kFxRange: u64 terms < 2^(kFxBits + kFxRange)
+constexpr float kFxBright = 16777216.0f;     // 2^kFxBits: segments with a larger peak take the global path
 constexpr float kFxLimit = 4294967040.0f;   // largest float below 2^32
-__device__ __forceinline__ int fx_exponent(unsigned amax_bits) {
-    const float a = __uint_as_float(amax_bits);
-    if (!(a > 0.f) || !(a < 3.0e38f)) return 0;
-    int e;
-    frexpf(a, &e);   // a < 2^e
-    e = kFxBits - e;
-    return e < -120 ? -120 : (e > 120 ? 120 : e);
-}
+constexpr int kFxBins = 256;                 // bound histogram: one bin per binary exponent (float bits >> 23)
+constexpr int kFxTailBytes = 2048;           // workspace tail of the FX area: bins u32 [256] | info int [8]
 // FX bank placement.  A ds_add_u64 is serviced in 4 groups of 16 lanes; two lanes of a group whose words lie
 // on the same bank pair (word index mod 16) serialize.  Every active lane advances 10 words per round, so the
 // pairs' residues within a group stay fixed for a segment's life: at refill a new segment may start up to
@@ -538,6 +544,13 @@ __device__ __forceinline__ void emit2(float2* at, float v0, float v1) {
         *at = x;
         __asm__ __volatile__("" ::: "memory");
     }
+}
+
+// FX bright segment: one value (in units, rounded to nearest; non-finite saturates) as a u64 integer add
+// into the wall point's global row (agent-scope atomic, no return)
+__device__ __forceinline__ void fx_gadd(unsigned long long* at, float v) {
+    const unsigned long long u = (unsigned long long)fminf(v + 0.5f, 1.8e19f);
+    __hip_atomic_fetch_add(at, u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // FX refill placement (see kFxShift): newl = this lane took a new segment, act = it holds one
@@ -611,10 +624,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
     const float rscale = k.opt.ray_scale;
     const int flags = k.opt.flags;
     // FX: log2 of the unit scale, folded into every pair's log2 amplitude; per-lane peak bookkeeping
-    const float fxE = FX ? (float)fx_exponent(*k.fx_amax) : 0.f;
+    const float fxE = FX ? (float)k.fx_info[0] : 0.f;
     const float fxS = FX ? fast_exp2(fxE) : 1.f;   // exact: fxE is an integer
     float fthr = kFxLimit / 64.f;   // wave-uniform
     float fpk = 0.f, fxs = 0.f;     // this lane's segment peak, and its peaks since the last check
+    bool brt = false;               // FX: this lane's segment is bright (global u64 adds, see kFxBits)
+    unsigned long long* const grow = FX ? k.hfx + (size_t)p * nr : nullptr;
     unsigned* hist32 = reinterpret_cast<unsigned*>(hist);
     const int nfx = nr + kSteps + 2;   // fields a round can reach (bins past nr are pad)
     // the float2 drain (two bins per LDS read-add-write; claim keys on bin pairs)
@@ -698,15 +713,21 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
                         // the segment's largest value (t = 0), in units (netf: T <= its start x (1 + 1e-7)^nr)
                         fpk = MODE == NLOSGR_MODE_NETF ? d.T * fast_exp2(d.al) * 1.001f
                                                        : fast_exp2(d.al) * (MODE == NLOSGR_MODE_BININT ? 1.001f : 1.f);
+                        brt = !(fpk < kFxBright);   // (non-finite peaks too)
+                        if (brt) fpk = 0.f;         // bright: no LDS adds
                         fxs += fpk;
                     }
                 }
                 nseg += NLOSGR_FCOUNT_ON ? 0u : (unsigned)__popcll(__builtin_amdgcn_ballot_w64(got));
+                if (FX) {
+                    const unsigned long long bm = __builtin_amdgcn_ballot_w64(take && act && brt);
+                    if (bm && lane == 0) atomicAdd(k.fx_info + 3, (int)__popcll(bm));
+                }
                 const int ntake = min(nidle, qcount);
                 qhead = (qhead + ntake) & (kRQ - 1);
                 qcount -= ntake;
                 // (netf keeps its start: its transmittance would have to be re-seeded)
-                if (FX && kFxShift > 0 && MODE != NLOSGR_MODE_NETF) fx_place(take && act, act, d);
+                if (FX && kFxShift > 0 && MODE != NLOSGR_MODE_NETF) fx_place(take && act && !brt, act && !brt, d);
             }
             const bool anyact = __builtin_amdgcn_ballot_w64(act) != 0;
             if (!anyact) {
@@ -726,6 +747,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
                 for (int t = lane; t < nfx; t += 64) mx = max(mx, hist32[t]);
                 for (int o2 = 32; o2 > 0; o2 >>= 1) mx = max(mx, (unsigned)__shfl_xor((int)mx, o2));
                 if (mx >= 0x80000000u) {
+                    if (lane == 0) atomicAdd(k.fx_info + 2, 1);
                     for (int t = lane; t < nfx; t += 64) {
                         const unsigned v = hist32[t];
                         if (v && t < nr)
@@ -764,28 +786,45 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
                 // per-step mask switching).
                 const int o = d.pos & (VW - 1);
                 const int lim = remw + o;   // slot j is in the segment iff o <= j < lim
+                // FX: bright lanes (brt) add into the wall point's global u64 row instead of the LDS; the
+                // rounds without one (all of them unless the bounds spread, see kFxBits) run the plain loop
+                const bool anyb = FX && __builtin_amdgcn_ballot_w64(win && brt) != 0ull;
+                const int gb0 = d.pos & ~(VW - 1);
+                auto emit_l = [&](int kv, float v0, float v1) { emit2<FX>(reinterpret_cast<float2*>(hb) + kv, v0, v1); };
+                auto emit_g = [&](int kv, float v0, float v1) {
+                    if (brt) {
+                        const int b = gb0 + VW * kv;
+                        if (b < nr && v0 > 0.f) fx_gadd(grow + b, v0);
+                        if (b + 1 < nr && v1 > 0.f) fx_gadd(grow + b + 1, v1);
+                    } else {
+                        emit2<FX>(reinterpret_cast<float2*>(hb) + kv, v0, v1);
+                    }
+                };
                 if (TAIL && win && MODE == NLOSGR_MODE_NOOCL) {
                     // the recurrence is seeded at pos (inside the support: a seed one bin further out can
                     // underflow for Gaussians much narrower than a bin); slot 0 before pos (o = 1) adds 0
                     float cur = fast_exp2(fmaf(d.ga, t * t, d.al));
                     float q = fast_exp2(d.ga * fmaf(2.f, t, 1.f));
                     const float cc = fast_exp2(2.f * d.ga);
-                    float2* hb2 = reinterpret_cast<float2*>(hb);
+                    auto run = [&](auto emit) {
 #pragma unroll
-                    for (int kv = 0; kv < kSteps / VW; ++kv) {
-                        const float v0 = (kv == 0 && o) ? 0.f : cur;
-                        if (kv == 0) {
-                            cur = o ? cur : cur * q;
-                            q = o ? q : q * cc;
-                        } else {
+                        for (int kv = 0; kv < kSteps / VW; ++kv) {
+                            const float v0 = (kv == 0 && o) ? 0.f : cur;
+                            if (kv == 0) {
+                                cur = o ? cur : cur * q;
+                                q = o ? q : q * cc;
+                            } else {
+                                cur *= q;
+                                q *= cc;
+                            }
+                            const float v1 = cur;
                             cur *= q;
                             q *= cc;
+                            emit(kv, v0, v1);
                         }
-                        const float v1 = cur;
-                        cur *= q;
-                        q *= cc;
-                        emit2<FX>(hb2 + kv, v0, v1);
-                    }
+                    };
+                    if (anyb) run(emit_g);
+                    else run(emit_l);
                 } else if (TAIL && win && MODE == NLOSGR_MODE_BININT) {
                     // bin-integrated (C4), TAIL: the average of exp(-beta^2 t^2) over the bin [t - 1/2, t + 1/2]
                     // (t in bins from the closest approach, beta = dr sqrt(a / 2)) is g(t) (1 + sum_n g^(2n)(t) /
@@ -805,29 +844,32 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
                     const bool series = d.beta <= kBetaSeries;
                     const bool anyerf = __builtin_amdgcn_ballot_w64(!series) != 0;   // (EXEC = the winners)
                     const float pref = fast_exp2(d.al) * (0.88622692545275801f * frcp(d.beta));
-                    float2* hb2 = reinterpret_cast<float2*>(hb);
+                    auto run = [&](auto emit) {
 #pragma unroll
-                    for (int kv = 0; kv < kSteps / VW; ++kv) {
-                        float v[VW];
+                        for (int kv = 0; kv < kSteps / VW; ++kv) {
+                            float v[VW];
 #pragma unroll
-                        for (int jj = 0; jj < VW; ++jj) {
-                            const int jslot = VW * kv + jj;
-                            const float tj = t0 + (float)jslot;
-                            const float u = b * tj * tj;
-                            float val = cur * fmaf(u, fmaf(u, fmaf(u, c3, c2), c1), c0);
-                            if (anyerf && !series) {
-                                const float x0 = d.beta * (tj - 0.5f), x1 = d.beta * (tj + 0.5f);
-                                const float e0 = erfcf(fabsf(x0)), e1 = erfcf(fabsf(x1));
-                                const float df = x0 >= 0.f ? e0 - e1 : (x1 <= 0.f ? e1 - e0 : 2.0f - e0 - e1);
-                                val = pref * df;
+                            for (int jj = 0; jj < VW; ++jj) {
+                                const int jslot = VW * kv + jj;
+                                const float tj = t0 + (float)jslot;
+                                const float u = b * tj * tj;
+                                float val = cur * fmaf(u, fmaf(u, fmaf(u, c3, c2), c1), c0);
+                                if (anyerf && !series) {
+                                    const float x0 = d.beta * (tj - 0.5f), x1 = d.beta * (tj + 0.5f);
+                                    const float e0 = erfcf(fabsf(x0)), e1 = erfcf(fabsf(x1));
+                                    const float df = x0 >= 0.f ? e0 - e1 : (x1 <= 0.f ? e1 - e0 : 2.0f - e0 - e1);
+                                    val = pref * df;
+                                }
+                                const bool pre = kv == 0 && jj < o;   // slot before pos (first round of a segment)
+                                v[jj] = pre ? 0.f : val;
+                                cur = pre ? cur : cur * q;
+                                q = pre ? q : q * cc;
                             }
-                            const bool pre = kv == 0 && jj < o;   // slot before pos (first round of a segment)
-                            v[jj] = pre ? 0.f : val;
-                            cur = pre ? cur : cur * q;
-                            q = pre ? q : q * cc;
+                            emit(kv, v[0], v[1]);
                         }
-                        emit2<FX>(hb2 + kv, v[0], v[1]);
-                    }
+                    };
+                    if (anyb) run(emit_g);
+                    else run(emit_l);
                 } else if (TAIL && win) {
                     // netf, TAIL: out_k = w c dT sin(theta) pdf_k T_k, T_{k+1} = T_k (exp(-sigma pdf_k c dT)
                     // + 1e-7), two bins per float2 read-add-write; slot 0 before pos (o = 1, a segment's
@@ -846,28 +888,31 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
                     const float sx = d.sc;
                     const float e1 = -sx * kRTf0, e2 = 0.5f * sx * sx * kRTf0, e3 = (-1.0f / 6.0f) * sx * sx * sx * kRTf0;
                     auto gfac = [e1, e2, e3](float pv) { return fmaf(pv, fmaf(pv, e3, e2), e1); };
-                    float2* hb2 = reinterpret_cast<float2*>(hb);
+                    auto run = [&](auto emit) {
 #pragma unroll
-                    for (int kv = 0; kv < kSteps / VW; ++kv) {
-                        const float p0 = cur;
-                        if (kv == 0) {
-                            cur = o ? cur : cur * q;
-                            q = o ? q : q * cc;
-                        } else {
+                        for (int kv = 0; kv < kSteps / VW; ++kv) {
+                            const float p0 = cur;
+                            if (kv == 0) {
+                                cur = o ? cur : cur * q;
+                                q = o ? q : q * cc;
+                            } else {
+                                cur *= q;
+                                q *= cc;
+                            }
+                            const float p1 = cur;
                             cur *= q;
                             q *= cc;
+                            // T carries w c dT sin(theta) (set at the segment's start); slot 0 before pos adds 0
+                            // and (v0 = 0) leaves T as it is
+                            const float v0 = (kv == 0 && o) ? 0.f : T * p0;
+                            T = fmaf(v0, gfac(p0), T);
+                            const float v1 = T * p1;
+                            T = fmaf(v1, gfac(p1), T);
+                            emit(kv, v0, v1);
                         }
-                        const float p1 = cur;
-                        cur *= q;
-                        q *= cc;
-                        // T carries w c dT sin(theta) (set at the segment's start); slot 0 before pos adds 0 and
-                        // (v0 = 0) leaves T as it is
-                        const float v0 = (kv == 0 && o) ? 0.f : T * p0;
-                        T = fmaf(v0, gfac(p0), T);
-                        const float v1 = T * p1;
-                        T = fmaf(v1, gfac(p1), T);
-                        emit2<FX>(hb2 + kv, v0, v1);
-                    }
+                    };
+                    if (anyb) run(emit_g);
+                    else run(emit_l);
                     T *= o ? kTfPow<kSteps - 1>() : kTfPow<kSteps>();   // T = T~ c0^(bins advanced)
                 } else if (win) {
                     float cur = fast_exp2(fmaf(d.ga, t * t, d.al));
@@ -1028,13 +1073,18 @@ __global__ __launch_bounds__(kBlock) void hist_reduce_kernel(const float* __rest
     hist[i] = s * att[t] * hscale[p];
 }
 
-// FX: the launch's amplitude bound max_g sigma_g * rho_max_g, rho_max = 0.5 + sum_l |f_l| sqrt((2l+1)/4pi)
+// FX: each Gaussian's amplitude bound b_g = sigma_g * rho_max_g, rho_max = 0.5 + sum_l |f_l| sqrt((2l+1)/4pi)
 // (Cauchy-Schwarz with sum_m Y_lm(d)^2 = (2l+1)/4pi on the unit sphere; 5 % margin for the cuda preset's
-// eps-shortened view direction), as float bits (non-negative floats order like their bits)
+// eps-shortened view direction), counted into a histogram of binary exponents (float bits >> 23; a
+// workgroup histogram in LDS first, then its non-empty bins into the global one).  Non-finite or zero
+// bounds are not counted: a NaN Gaussian is skipped by the drains (w > 0 fails) and must not move the unit
+// of the others; an infinite one takes the bright path (saturating, kFxBits).
 template <int PRESET>
-__global__ __launch_bounds__(kBlock) void fx_amax_kernel(nlosgr_gaussians g, float ascale, unsigned* amax) {
+__global__ __launch_bounds__(kBlock) void fx_bound_kernel(nlosgr_gaussians g, float ascale, unsigned* bins) {
+    __shared__ unsigned lh[kFxBins];
+    lh[threadIdx.x] = 0u;
+    __syncthreads();
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    float a = 0.f;
     if (i < g.ng) {
         const float sig = 1.0f / (1.0f + expf(-g.opacity[i]));
         const float* f = g.features + (size_t)i * g.k_feat;
@@ -1045,24 +1095,60 @@ __global__ __launch_bounds__(kBlock) void fx_amax_kernel(nlosgr_gaussians g, flo
             for (int c = l * l; c < (l + 1) * (l + 1) && c < g.k_feat; ++c) n2 += f[c] * f[c];
             sh += sqrtf(n2) * sqrtf((2.0f * l + 1.0f) * (0.25f / kPi));
         }
-        a = sig * (0.5f + 1.05f * sh) * 1.001f * ascale;   // ascale: the mode's factor (netf: c dT)
-        if (!(a >= 0.f)) a = __uint_as_float(0x7f800000u);   // NaN parameters: E = 0
+        const float a = sig * (0.5f + 1.05f * sh) * 1.001f * ascale;   // ascale: the mode's factor (netf: c dT)
+        if (a > 0.f && a < 3.0e38f) atomicAdd(&lh[__float_as_uint(a) >> 23], 1u);
     }
-    unsigned b = __float_as_uint(a);
-    for (int o = 32; o > 0; o >>= 1) b = max(b, (unsigned)__shfl_xor((int)b, o));
-    if (lane_id() == 0) atomicMax(amax, b);
+    __syncthreads();
+    const unsigned c = lh[threadIdx.x];
+    if (c) atomicAdd(bins + threadIdx.x, c);
+}
+
+// FX: the unit exponent from the bound histogram (one workgroup).  e_q = the largest exponent bin with at
+// least ceil(n / 256) counted bounds at or above it (bin e holds bounds in [2^(e-127), 2^(e-126))), so
+// fewer than ceil(n / 256) Gaussians have a bound above 2^(e_q - 126); E = kFxBits - (e_q - 126) puts that
+// bound below 2^kFxBits units.  E <= E(top bin) + kFxRange.  info[0] = E, info[1] = E of the top bin.
+__global__ __launch_bounds__(kFxBins) void fx_unit_kernel(const unsigned* __restrict__ bins, int* info, int maxunit) {
+    __shared__ unsigned cum[kFxBins];
+    const int t = threadIdx.x;
+    cum[t] = bins[t];
+    __syncthreads();
+    for (int off = 1; off < kFxBins; off <<= 1) {   // suffix sums: cum[e] = sum_{e' >= e} bins[e']
+        const unsigned v = t + off < kFxBins ? cum[t + off] : 0u;
+        __syncthreads();
+        cum[t] += v;
+        __syncthreads();
+    }
+    const unsigned n = cum[0];
+    const unsigned kq = (n + 255u) / 256u;
+    // the largest e with cum[e] >= kq (resp. >= 1 for the top bin): cum is non-increasing in e
+    const bool q = n > 0u && cum[t] >= kq && (t + 1 == kFxBins || cum[t + 1] < kq);
+    const bool top = n > 0u && cum[t] >= 1u && (t + 1 == kFxBins || cum[t + 1] < 1u);
+    __shared__ int eq, et;
+    if (t == 0) { eq = 0; et = 0; }
+    __syncthreads();
+    if (q) eq = t;
+    if (top) et = t;
+    __syncthreads();
+    if (t == 0) {
+        auto unit = [](int e) { const int u = kFxBits - (e - 126); return u < -120 ? -120 : (u > 120 ? 120 : u); };
+        const int emax = n > 0u ? unit(et) : 0;
+        int e = n > 0u ? unit(maxunit ? et : eq) : 0;   // maxunit: round 5's rule (diagnostics)
+        if (e > emax + kFxRange) e = emax + kFxRange;
+        info[0] = e;
+        info[1] = emax;
+    }
 }
 
 // FX: hist[p,t] = (u64 count x 2^-E) x att[t] x hscale[p]
 __global__ __launch_bounds__(kBlock) void fx_reduce_kernel(const unsigned long long* __restrict__ hfx,
-                                                           const unsigned* __restrict__ amax, long long P, int nr,
+                                                           const int* __restrict__ info, long long P, int nr,
                                                            const float* __restrict__ att,
                                                            const float* __restrict__ hscale, float* __restrict__ hist) {
     const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= P * nr) return;
     const long long p = i / nr;
     const int t = (int)(i - p * nr);
-    const double q = ldexp(1.0, -fx_exponent(*amax));
+    const double q = ldexp(1.0, -info[0]);
     hist[i] = (float)((double)hfx[i] * q) * att[t] * hscale[p];
 }
 
@@ -2054,7 +2140,7 @@ __global__ __launch_bounds__(kBlock) void bbox_kernel(nlosgr_gaussians g, float 
 // host side
 // ------------------------------------------------------------------------------------------
 
-bool bwd_shared(const nlosgr_geometry* geo);
+bool bwd_shared(const nlosgr_geometry* geo, const nlosgr_options* opt);
 
 int validate(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_options* opt) {
     if (!g || !geo || !opt) return set_err(NLOSGR_E_INVALID, "null argument struct");
@@ -2084,16 +2170,16 @@ int validate(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr
         return set_err(NLOSGR_E_INVALID, "null geometry pointer");
     if (tiles_engine(opt)) return tiles_validate(g, geo, opt);
     const size_t lds_f = (size_t)FwdLayout(geo->nr, geo->nt, geo->np).total * 4;
-    const size_t lds_b = (size_t)BwdLayout(geo->nr, geo->nt, geo->np, bwd_shared(geo)).total * 4;
+    const size_t lds_b = (size_t)BwdLayout(geo->nr, geo->nt, geo->np, bwd_shared(geo, opt)).total * 4;
     if (lds_f > 160 * 1024 || lds_b > 160 * 1024) return set_err(NLOSGR_E_UNSUPPORTED, "problem exceeds LDS budget");
     return NLOSGR_OK;
 }
 
 // shared-row backward layout when per-wave rows would leave fewer than 4 workgroups per CU
-// (long rows, e.g. C5's 2048 bins); NLOSGR_BSHARED=0/1 forces either layout (A/B timing)
-bool bwd_shared(const nlosgr_geometry* geo) {
-    const char* e = getenv("NLOSGR_BSHARED");
-    if (e && (e[0] == '0' || e[0] == '1')) return e[0] == '1';
+// (long rows, e.g. C5's 2048 bins); NLOSGR_FLAG_BWD_SHARED / _PERWAVE force either layout (A/B timing)
+bool bwd_shared(const nlosgr_geometry* geo, const nlosgr_options* opt) {
+    if (opt->flags & NLOSGR_FLAG_BWD_SHARED) return true;
+    if (opt->flags & NLOSGR_FLAG_BWD_PERWAVE) return false;
     return (size_t)BwdLayout(geo->nr, geo->nt, geo->np).total * 4 > 40 * 1024;
 }
 
@@ -2153,10 +2239,10 @@ void launch_fwd(const KArgs& ka, size_t shm, hipStream_t s) {
     }
     constexpr bool kCanTail = (MODE == NLOSGR_MODE_NOOCL || MODE == NLOSGR_MODE_NETF || MODE == NLOSGR_MODE_BININT) &&
                               !DENSE && !RAYS;
-    // NLOSGR_FTAIL=0: masked forward drain at every cutoff (A/B and parity cross-check); netf takes the
-    // TAIL drain where its backward does (c dT <= 1/64), so both see the same support
-    const char* ftail = getenv("NLOSGR_FTAIL");
-    const bool tail = kCanTail && ka.opt.cutoff >= kTailCutoff && (!ka.counts || NLOSGR_FCOUNT_ON) && !(ftail && ftail[0] == '0') &&
+    // NLOSGR_FLAG_MASKED_FWD: masked forward drain at every cutoff (A/B and parity cross-check); netf takes
+    // the TAIL drain where its backward does (c dT <= 1/64), so both see the same support
+    const bool tail = kCanTail && ka.opt.cutoff >= kTailCutoff && (!ka.counts || NLOSGR_FCOUNT_ON) &&
+                      !(ka.opt.flags & NLOSGR_FLAG_MASKED_FWD) &&
                       (MODE != NLOSGR_MODE_NETF || ka.opt.c_deltaT <= kSmallX);
     if (tail) hipLaunchKernelGGL((fwd_kernel<PRESET, MODE, DENSE, RAYS, CACHE, kCanTail>), grid, dim3(kBlock), shm, s, ka);
     else hipLaunchKernelGGL((fwd_kernel<PRESET, MODE, DENSE, RAYS, CACHE>), grid, dim3(kBlock), shm, s, ka);
@@ -2166,8 +2252,8 @@ void launch_bwd(const KArgs& ka, size_t shm, hipStream_t s) {
     const int gpb = ka.bshared ? kNB * kWaves : kNB;
     dim3 grid((ka.g_hi - ka.g_lo + gpb - 1) / gpb, ka.nsplit);
     constexpr bool kCanTail = (MODE == NLOSGR_MODE_NOOCL || MODE == NLOSGR_MODE_NETF) && !DENSE && !RAYS;
-    const char* bt = getenv("NLOSGR_BTAIL");   // NLOSGR_BTAIL=0: masked backward drains (A/B, parity cross-check)
-    const bool tail = kCanTail && ka.opt.cutoff >= kTailCutoff && !(bt && bt[0] == '0') &&
+    // NLOSGR_FLAG_MASKED_BWD: masked backward drains (A/B, parity cross-check)
+    const bool tail = kCanTail && ka.opt.cutoff >= kTailCutoff && !(ka.opt.flags & NLOSGR_FLAG_MASKED_BWD) &&
                       (MODE != NLOSGR_MODE_NETF || ka.opt.c_deltaT <= kSmallX);
     if (ka.bshared) {
         if (tail) hipLaunchKernelGGL((bwd_kernel<PRESET, MODE, DENSE, RAYS, CACHE, true, kCanTail>), grid, dim3(kBlock), shm, s, ka);
@@ -2227,22 +2313,20 @@ int fwd_nsplit(const nlosgr_gaussians* g, const nlosgr_geometry* geo) {
     return ns < 1 ? 1 : ns;
 }
 // forward partials: float [nfsplit][P][nr] (float drains) or, for the FX drain, u64 [P][nr] + the
-// amplitude-bound word at the end
+// bound histogram and info words (kFxTailBytes) at the end
 size_t fpart_bytes(const nlosgr_gaussians* g, const nlosgr_geometry* geo) {
     const int ns = fwd_nsplit(g, geo);
     const size_t fl = ns > 1 ? (size_t)ns * geo->nwall * geo->nr * sizeof(float) : 0;
     const size_t fx = (size_t)geo->nwall * geo->nr * sizeof(unsigned long long);
-    return align_up(fl > fx ? fl : fx) + 256;
+    return align_up(fl > fx ? fl : fx) + kFxTailBytes;
 }
 // the fixed-point TAIL drain serves the culled no-occlusion histogram at cutoff >= kTailCutoff
-// (NLOSGR_FFX=0: the float claim drain instead, A/B)
+// (NLOSGR_FLAG_FLOAT_DRAIN: the float claim drain instead, A/B)
 bool fx_eligible(const nlosgr_options* opt, bool dense, bool rays, bool counts, bool hist, bool cache) {
-    const char* e = getenv("NLOSGR_FFX");
-    const char* ft = getenv("NLOSGR_FTAIL");
     const bool mode_ok = opt->mode == NLOSGR_MODE_NOOCL || opt->mode == NLOSGR_MODE_BININT ||
                          (opt->mode == NLOSGR_MODE_NETF && opt->c_deltaT <= kSmallX);   // (the TAIL drains)
     return mode_ok && opt->cutoff >= kTailCutoff && !dense && !rays && !counts && hist && !cache &&
-           !(e && e[0] == '0') && !(ft && ft[0] == '0');
+           !(opt->flags & (NLOSGR_FLAG_FLOAT_DRAIN | NLOSGR_FLAG_MASKED_FWD));
 }
 // after the ray cache: drho [P][ng] | sh partials [nsh][ng][kShPart] | 256-B diagnostics tail |
 // forward split partial histograms [nfsplit][P][nr]
@@ -2250,6 +2334,12 @@ size_t sh_bytes(const nlosgr_gaussians* g, const nlosgr_geometry* geo0) {
     const nlosgr_geometry gb = batch_geo(g, geo0);   // dL/drho for one wall-point batch
     return align_up((size_t)gb.nwall * g->ng * sizeof(float)) +
            align_up((size_t)sh_nsplit(g, &gb) * g->ng * kShPart * sizeof(float));
+}
+// the forward partials / FX area (after the backward buffers and the 256-B diagnostics tail)
+char* fpart_ptr(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_options* opt, void* workspace) {
+    return (char*)workspace + align_up((size_t)g->ng * sizeof(GaussRec)) +
+           align_up((size_t)bwd_nsplit_ws(g, geo, opt) * g->ng * 32 * sizeof(float)) + cache_bytes(g, geo, opt) +
+           sh_bytes(g, geo) + 256;
 }
 void cache_ptrs(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_options* opt, void* ws, int nsplit,
                 KArgs& ka) {
@@ -2273,24 +2363,24 @@ int run_fwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_
     const int nfs = fwd_nsplit(g, geo);
     const bool dense = !(opt->cutoff > 0.f);
     const bool rays = ray_out != nullptr;
-    char* fpart = g->ng > 0 ? (char*)workspace + align_up((size_t)g->ng * sizeof(GaussRec)) +
-                                  align_up((size_t)bwd_nsplit_ws(g, geo, opt) * g->ng * 32 * sizeof(float)) +
-                                  cache_bytes(g, geo, opt) + sh_bytes(g, geo) + 256
-                            : nullptr;
+    char* fpart = g->ng > 0 ? fpart_ptr(g, geo, opt, workspace) : nullptr;
     const bool fx = g->ng > 0 && fx_eligible(opt, dense, rays, counts != nullptr, hist_out != nullptr, ka.cmask != nullptr);
     if (fx) {
         ka.hfx = (unsigned long long*)fpart;
-        unsigned* amax = (unsigned*)(fpart + fpart_bytes(g, geo) - 256);
-        ka.fx_amax = amax;
+        unsigned* bins = (unsigned*)(fpart + fpart_bytes(g, geo) - kFxTailBytes);
+        ka.fx_info = (int*)(bins + kFxBins);
         ka.nfsplit = nfs;
         HIPCHK(hipMemsetAsync(ka.hfx, 0, (size_t)geo->nwall * geo->nr * sizeof(unsigned long long), s));
-        HIPCHK(hipMemsetAsync(amax, 0, sizeof(unsigned), s));
+        HIPCHK(hipMemsetAsync(bins, 0, kFxBins * sizeof(unsigned) + 8 * sizeof(int), s));
         const int nb = (g->ng + kBlock - 1) / kBlock;
         const float ascale = opt->mode == NLOSGR_MODE_NETF ? opt->c_deltaT : 1.0f;
         if (g->preset == NLOSGR_PRESET_TORCH)
-            hipLaunchKernelGGL(fx_amax_kernel<NLOSGR_PRESET_TORCH>, dim3(nb), dim3(kBlock), 0, s, *g, ascale, amax);
+            hipLaunchKernelGGL(fx_bound_kernel<NLOSGR_PRESET_TORCH>, dim3(nb), dim3(kBlock), 0, s, *g, ascale, bins);
         else
-            hipLaunchKernelGGL(fx_amax_kernel<NLOSGR_PRESET_CUDA>, dim3(nb), dim3(kBlock), 0, s, *g, ascale, amax);
+            hipLaunchKernelGGL(fx_bound_kernel<NLOSGR_PRESET_CUDA>, dim3(nb), dim3(kBlock), 0, s, *g, ascale, bins);
+        HIPCHK(hipGetLastError());
+        hipLaunchKernelGGL(fx_unit_kernel, dim3(1), dim3(kFxBins), 0, s, bins, ka.fx_info,
+                           (opt->flags & NLOSGR_FLAG_FX_MAXUNIT) ? 1 : 0);
         HIPCHK(hipGetLastError());
     } else if (hist_out && nfs > 1 && g->ng > 0) {
         ka.hpart = (float*)fpart;
@@ -2301,10 +2391,9 @@ int run_fwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_
         HIPCHK(hipGetLastError());
     }
     const size_t shm = (size_t)FwdLayout(geo->nr, geo->nt, geo->np, fx).total * sizeof(float);
-    // NLOSGR_FDREG=0 routes the dense histogram through fwd_kernel instead (parity cross-check in tests)
-    const char* fdreg = getenv("NLOSGR_FDREG");
+    // NLOSGR_FLAG_LANE_DENSE routes the dense histogram through fwd_kernel instead (parity cross-check)
     if (dense && !rays && !counts && hist_out && opt->mode == NLOSGR_MODE_NOOCL && geo->nr <= 1024 &&
-        !(fdreg && fdreg[0] == '0')) {
+        !(opt->flags & NLOSGR_FLAG_LANE_DENSE)) {
         // dense no-occlusion histogram: lane = bin register accumulation (fwd_dense_kernel)
         if (g->ng > 0 && geo->nwall > 0) {
             const size_t shd = (size_t)FwdDenseLayout(geo->nr, geo->nt, geo->np).total * sizeof(float);
@@ -2347,7 +2436,7 @@ int run_fwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_
     if (ka.hfx) {
         const long long n = (long long)geo->nwall * geo->nr;
         hipLaunchKernelGGL(fx_reduce_kernel, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, ka.hfx,
-                           ka.fx_amax, (long long)geo->nwall, geo->nr, geo->att, geo->hscale, hist_out);
+                           ka.fx_info, (long long)geo->nwall, geo->nr, geo->att, geo->hscale, hist_out);
         HIPCHK(hipGetLastError());
     } else if (ka.hpart) {
         const long long n = (long long)geo->nwall * geo->nr;
@@ -2403,6 +2492,18 @@ int nlosgr_render_fwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo, con
     return run_fwd(g, geo, opt, workspace, hist_out, ray_out, nullptr, (hipStream_t)hip_stream);
 }
 
+int nlosgr_fx_info(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_options* opt,
+                   const void* workspace, int32_t* info_out, void* hip_stream) {
+    const int rc = validate(g, geo, opt);
+    if (rc) return rc;
+    if (!workspace || !info_out) return set_err(NLOSGR_E_INVALID, "null workspace or info_out");
+    if (tiles_engine(opt) || g->ng == 0) return set_err(NLOSGR_E_UNSUPPORTED, "fx_info: pair-major forward with ng > 0");
+    const char* fpart = fpart_ptr(g, geo, opt, const_cast<void*>(workspace));
+    const char* info = fpart + fpart_bytes(g, geo) - kFxTailBytes + kFxBins * sizeof(unsigned);
+    HIPCHK(hipMemcpyAsync(info_out, info, 4 * sizeof(int32_t), hipMemcpyDeviceToDevice, (hipStream_t)hip_stream));
+    return NLOSGR_OK;
+}
+
 int nlosgr_count_support(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_options* opt,
                          void* workspace, unsigned long long* counts, void* hip_stream) {
     const int rc = validate(g, geo, opt);
@@ -2443,7 +2544,7 @@ int nlosgr_render_bwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo, con
     ka.grad_hist = grad_hist; ka.grad_ray = grad_ray;
     ka.g_lo = opt->g_end > 0 ? opt->g_begin : 0;
     ka.g_hi = opt->g_end > 0 ? opt->g_end : g->ng;
-    ka.bshared = bwd_shared(geo) ? 1 : 0;
+    ka.bshared = bwd_shared(geo, opt) ? 1 : 0;
     const nlosgr_geometry gbat = batch_geo(g, geo);
     ka.nsplit = bwd_nsplit(g, &gbat, opt, ka.bshared != 0);
     cache_ptrs(g, geo, opt, workspace, bwd_nsplit_ws(g, geo, opt), ka);

@@ -59,10 +59,19 @@ class AdamGroup(ctypes.Structure):
 
 ADAM_MAX_GROUPS = 8  # NLOSGR_ADAM_MAX_GROUPS
 MAX_PER_RAY = 256   # NLOSGR_MAX_PER_RAY
-ABI_VERSION = 7     # NLOSGR_ABI_VERSION
+ABI_VERSION = 8     # NLOSGR_ABI_VERSION
+
+# nlosgr_options.flags variant selection (NLOSGR_FLAG_*; A/B timing and parity cross-checks, 0 in production)
+FLAG_FLOAT_DRAIN = 0x100   # forward: fp32 claim drain instead of the fixed-point drain
+FLAG_MASKED_FWD = 0x200    # forward: masked drains at every cutoff (no TAIL)
+FLAG_MASKED_BWD = 0x400    # backward: masked drains at every cutoff (no TAIL)
+FLAG_LANE_DENSE = 0x800    # dense no-occlusion histogram through the lane-serial drain
+FLAG_BWD_SHARED = 0x1000   # backward: shared-row layout
+FLAG_BWD_PERWAVE = 0x2000  # backward: per-wave row layout
+FLAG_FX_MAXUNIT = 0x4000   # FX drain unit from the largest bound (round-5 rule; diagnostics)
 
 # every symbol include/nlosgr.h declares (tests check the exports against this list)
-EXPORTS = ["nlosgr_workspace_bytes", "nlosgr_render_fwd", "nlosgr_render_bwd", "nlosgr_count_support",
+EXPORTS = ["nlosgr_workspace_bytes", "nlosgr_render_fwd", "nlosgr_render_bwd", "nlosgr_count_support", "nlosgr_fx_info",
            "nlosgr_bboxes", "nlosgr_rays_workspace_bytes", "nlosgr_filter_rays", "nlosgr_rays_fwd",
            "nlosgr_rays_bwd", "nlosgr_rays_analytic", "nlosgr_mse_workspace_bytes", "nlosgr_mse", "nlosgr_adam",
            "nlosgr_carve_votes", "nlosgr_set_batch_budgets", "nlosgr_get_batch_budgets", "nlosgr_last_error", "nlosgr_abi_version"]
@@ -89,6 +98,8 @@ def load():
     lib.nlosgr_render_bwd.restype = ctypes.c_int
     lib.nlosgr_count_support.argtypes = [PG, PGEO, POPT, _P, _P, _P]
     lib.nlosgr_count_support.restype = ctypes.c_int
+    lib.nlosgr_fx_info.argtypes = [PG, PGEO, POPT, _P, _P, _P]
+    lib.nlosgr_fx_info.restype = ctypes.c_int
     PR = ctypes.POINTER(Rays)
     lib.nlosgr_rays_workspace_bytes.argtypes = [PG, PR]
     lib.nlosgr_rays_workspace_bytes.restype = ctypes.c_size_t

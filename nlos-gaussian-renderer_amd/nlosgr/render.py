@@ -37,7 +37,7 @@ class RenderConfig:
     c_deltaT: float = 1.0
     ray_scale: float = 1.0
     nsplit: int = 0
-    flags: int = 0               # ablation / diagnostics only (0 in production)
+    flags: int = 0               # 0 in production; _lib.FLAG_* select A/B variants, bits 0-6 phase ablation
     ray_cache: bool = True       # forward records in-support rays per pair for the backward
     selection: str = "support"   # "support" (Mahalanobis cutoff) or "aabb" (path C's 3-sigma box filter,
                                  # first 256 Gaussians per ray by index; cuda preset)
@@ -151,6 +151,26 @@ def render_backward(mu, scaling, rotation, opacity, features, geo, cfg, grad_his
                                      _lib.ptr(d_s), _lib.ptr(d_q), _lib.ptr(d_o), _lib.ptr(d_f),
                                      _lib.stream_handle(dev)))
     return d_mu, d_s, d_q, d_o, d_f
+
+
+def fx_info(mu, scaling, rotation, opacity, features, geo, cfg, workspace):
+    """The fixed-point forward's state after render_forward(..., workspace=workspace) with the same inputs:
+    (E, E of the largest amplitude bound, LDS flushes, bright segments); zeros when the forward did not
+    take the fixed-point drain (nlosgr_fx_info)."""
+    lib = _lib.load()
+    dev = mu.device
+    mu, scaling, rotation, opacity, features = [_as_f32(t) for t in (mu, scaling, rotation, opacity, features)]
+    g, gs, o = _structs(mu, scaling, rotation, opacity, features, geo, cfg)
+    out = torch.zeros(4, dtype=torch.int32, device=dev)
+    _lib.check(lib.nlosgr_fx_info(g, gs, o, _lib.ptr(workspace), _lib.ptr(out), _lib.stream_handle(dev)))
+    return tuple(int(v) for v in out.cpu())
+
+
+def workspace_for(mu, scaling, rotation, opacity, features, geo, cfg, ray_cache=False):
+    """A workspace tensor sized for these inputs (nlosgr_workspace_bytes)."""
+    lib = _lib.load()
+    g, gs, o = _structs(*[_as_f32(t) for t in (mu, scaling, rotation, opacity, features)], geo, cfg, ray_cache)
+    return _workspace(lib, g, gs, o, mu.device)
 
 
 def count_support(mu, scaling, rotation, opacity, features, geo, cfg):

@@ -110,13 +110,14 @@ def allreduce_step(grads, loss4, n_total, group=None, async_op=False):
     return finish()
 
 
-def wall_centroid(wall, group=None):
+def wall_centroid(wall, group=None, reduce=True):
     """Centroid of the WHOLE relay wall.  With a wall shard per rank (world > 1) the sum and count of
-    every rank's wall points are all-reduced, so every rank gets the same centroid (slab_order's axis
-    must not depend on which band a rank renders)."""
+    every rank's wall points are all-reduced over `group`, so every rank gets the same centroid
+    (slab_order's axis must not depend on which band a rank renders).  reduce=False: this wall only,
+    no collective (a caller whose group has one rank must not all-reduce over the default group)."""
     w = wall.detach().reshape(-1, 3).double()
     s = torch.cat([w.sum(0), torch.tensor([float(w.shape[0])], dtype=torch.float64, device=w.device)])
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+    if reduce and dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
         dist.all_reduce(s, op=dist.ReduceOp.SUM, group=group)
     return (s[:3] / s[3].clamp_min(1.0)).float()
 
@@ -240,10 +241,9 @@ class TrainStep:
                  group=None, sh_schedule=False, events=None, buckets=4, keep_grads=False, bwd_order="slab",
                  fwd_order="slab"):
         self.model, self.geo, self.cfg = model, geo, cfg
-        # backward / forward Gaussian orders (slab_order; None = as stored); NLOSGR_BWD_ORDER=0 and
-        # NLOSGR_FWD_ORDER=0 disable them (A/B)
-        self.bwd_order = None if os.environ.get("NLOSGR_BWD_ORDER") == "0" else bwd_order
-        self.fwd_order = None if os.environ.get("NLOSGR_FWD_ORDER") == "0" else fwd_order
+        # backward / forward Gaussian orders (slab_order; None = as stored)
+        self.bwd_order = bwd_order
+        self.fwd_order = fwd_order
         self.keep_grads = keep_grads   # tests: keep the last step's (all-reduced) gradients in self.grads,
         self.grads = None              # its forward volume in self.hist and its dL/dhist in self.grad_hist
         self.hist = self.grad_hist = None
@@ -267,7 +267,7 @@ class TrainStep:
         self._batch_events = []
         self._occl_plan = None           # occlusion mode: wall-point batches, planned at the first step
         # the slab orders' axis comes from the whole wall's centroid (the same on every rank)
-        self.wall_c = wall_centroid(geo.wall, group) if self.world > 1 else wall_centroid(geo.wall)
+        self.wall_c = wall_centroid(geo.wall, group, reduce=self.world > 1)
         ng = model._mu.shape[0]
         self._tensors = [model._mu.data, model._features_dc.data.view(ng, -1), model._features_rest.data.view(ng, -1),
                          model._opacity.data.view(ng), model._scaling.data, model._rotation.data]
@@ -349,8 +349,13 @@ class TrainStep:
                 evs[0].record(stream)
             cached = self._occl_cache
             if cached:
-                hist, _, ws = render_forward(*params, geo, cfg, True, False, ray_cache=True)
-            else:
+                try:
+                    hist, _, ws = render_forward(*params, geo, cfg, True, False, ray_cache=True)
+                except torch.cuda.OutOfMemoryError:
+                    # the planned row cache did not fit after all (the caching allocator's free blocks
+                    # counted in occl_batches may be fragmented): recompute from here on
+                    self._occl_cache = cached = False
+            if not cached:
                 (hist, _), ws = render_forward(*params, geo, cfg, True, False), None
             if evs:
                 evs[1].record(stream)
@@ -415,12 +420,8 @@ class TrainStep:
         # indexed by the forward's order); its gradients are scattered back below
         perm = None
         if self.bwd_order == "slab" and not cache and cfg.mode != "occl" and cfg.selection == "support" and ng > 64:
-            sl = os.environ.get("NLOSGR_SLAB")   # A/B knobs: "slabs,cells" (default 8,4); size key 0 = off,
-            sc = tuple(int(v) for v in sl.split(",")) if sl else (8, 4)   # 1 = max log-scale, 2 = log-volume
-            sz = os.environ.get("NLOSGR_SLAB_SIZE", "1")
-            size = args[1].max(1).values if sz == "1" else (args[1].sum(1) if sz == "2" else None)
-            perm = slab_order(args[0], None, *sc, size=size,
-                              size_buckets=int(os.environ.get("NLOSGR_SLAB_SIZEB", "0")), centroid=self.wall_c)
+            # 8 slabs x 4 x 4 cells, largest log-scale within a cell (grid and key A/B'd in round 4)
+            perm = slab_order(args[0], None, 8, 4, size=args[1].max(1).values, centroid=self.wall_c)
             args = tuple(t[perm].contiguous() for t in args[:5]) + (args[5],)
 
         def unperm(gs):

@@ -188,11 +188,11 @@ def test_c3_full_size_train_step_parity():
         _close(a, b, 2e-4, atol=1e-9, msg=f"C3 subset grad {name}")
 
 
-def test_c3_trainstep_full_ng_accuracy(monkeypatch):
+def test_c3_trainstep_full_ng_accuracy():
     """The headline's accuracy at full Ng through the exact path bench.py times: one C3 TrainStep
     (default slab-ordered forward and backward, 5.7 sigma) with keep_grads.
       * forward rows of 2 wall points vs the float64 sum of 400 HIP sub-histograms of 250 Gaussians each
-        (float claim drain, NLOSGR_FFX=0: a few hundred terms per bin per sub-histogram), same geometry
+        (float claim drain, FLAG_FLOAT_DRAIN: a few hundred terms per bin per sub-histogram), same geometry
         and cutoff: max error <= 2e-5 of the rows' max (gaussian_model.py:346-364, nlos_helpers.py:228-229
         sum over all Gaussians);
       * all six gradients vs the unordered render_backward seeded with the step's own dL/dhist, on the
@@ -223,13 +223,14 @@ def test_c3_trainstep_full_ng_accuracy(monkeypatch):
             t.copy_(b)
     idx = torch.tensor([128 * 40 + 30, 128 * 100 + 90], device=dev)
     gsel = scene.geometry(dev, "cuda", "noocl", walls=geo.wall[idx].contiguous())
-    monkeypatch.setenv("NLOSGR_FFX", "0")
+    from dataclasses import replace
+    from nlosgr import _lib
     ref = torch.zeros(len(idx), T, dtype=torch.float64, device=dev)
     for g0 in range(0, ng, 250):
         sub = _subset(m, torch.arange(g0, min(ng, g0 + 250), device=dev))
-        h, _ = render_forward(*_params(sub), gsel, make_config(sub, scene, "cuda", "noocl", cutoff=PARITY_CUTOFF))
+        h, _ = render_forward(*_params(sub), gsel, replace(make_config(sub, scene, "cuda", "noocl", cutoff=PARITY_CUTOFF),
+                                                           flags=_lib.FLAG_FLOAT_DRAIN))
         ref += h.double()
-    monkeypatch.delenv("NLOSGR_FFX")
     a = hist[idx].double()
     err = float((a - ref).abs().max() / ref.abs().max())
     rel2 = float((a - ref).norm() / ref.norm())

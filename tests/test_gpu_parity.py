@@ -248,9 +248,9 @@ def test_ray_cache_backward_matches_uncached(mode):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("mode", ["noocl", "netf"])
-def test_bwd_shared_layout_matches_per_wave(mode, monkeypatch):
+def test_bwd_shared_layout_matches_per_wave(mode):
     """The shared-row backward layout (4 waves own 256 Gaussians and share each wall point's
-    staged row; chosen automatically for long rows, NLOSGR_BSHARED forces it) gives the per-wave
+    staged row; chosen automatically for long rows, FLAG_BWD_SHARED forces it) gives the per-wave
     layout's gradients within fp32 summation-order noise, with and without the ray cache, for a
     ragged Gaussian count and a workspace allocated under the other layout."""
     from nlosgr import GaussianParams, features_flat
@@ -264,11 +264,13 @@ def test_bwd_shared_layout_matches_per_wave(mode, monkeypatch):
     args = (m._mu.detach(), m._scaling.detach(), m._rotation.detach(), m._opacity.detach(),
             features_flat(m).detach().contiguous(), geo)
     g = torch.randn((scene.H * scene.W, scene.T), generator=torch.Generator().manual_seed(8)).to(dev) * 1e-3
-    monkeypatch.setenv("NLOSGR_BSHARED", "0")
+    from dataclasses import replace
+    from nlosgr import _lib
+    cfg = replace(cfg, flags=_lib.FLAG_BWD_PERWAVE)
     h0, _, ws = render_forward(*args, cfg, ray_cache=True)
     ref = render_backward(*args, cfg, grad_hist=g)
     ref_c = render_backward(*args, cfg, grad_hist=g, workspace=ws, ray_cache=True)
-    monkeypatch.setenv("NLOSGR_BSHARED", "1")
+    cfg = replace(cfg, flags=_lib.FLAG_BWD_SHARED)
     got = render_backward(*args, cfg, grad_hist=g)
     got_c = render_backward(*args, cfg, grad_hist=g, workspace=ws, ray_cache=True)   # ws from the other layout
     h1, _, ws1 = render_forward(*args, cfg, ray_cache=True)
@@ -284,9 +286,9 @@ def test_bwd_shared_layout_matches_per_wave(mode, monkeypatch):
 
 @pytest.mark.parametrize("preset", ["torch", "cuda"])
 @pytest.mark.parametrize("T", [40, 200])
-def test_dense_register_forward_matches_lane_serial(preset, T, monkeypatch):
+def test_dense_register_forward_matches_lane_serial(preset, T):
     """Dense no-occlusion histograms: the lane = bin register kernel (fwd_dense_kernel, default)
-    equals the lane-serial drain (NLOSGR_FDREG=0) within fp32 summation-order noise, for ragged
+    equals the lane-serial drain (FLAG_LANE_DENSE) within fp32 summation-order noise, for ragged
     bin and Gaussian counts and several Gaussian splits per wall point."""
     from nlosgr import GaussianParams, features_flat
     from nlosgr.volume import Scene, make_config
@@ -298,9 +300,9 @@ def test_dense_register_forward_matches_lane_serial(preset, T, monkeypatch):
     cfg = make_config(m, scene, preset, cutoff=0.0)
     args = (m._mu.detach(), m._scaling.detach(), m._rotation.detach(), m._opacity.detach(),
             features_flat(m).detach().contiguous(), geo)
-    monkeypatch.delenv("NLOSGR_FDREG", raising=False)
+    from dataclasses import replace
+    from nlosgr import _lib
     h_reg, _ = render_forward(*args, cfg)
-    monkeypatch.setenv("NLOSGR_FDREG", "0")
-    h_ser, _ = render_forward(*args, cfg)
+    h_ser, _ = render_forward(*args, replace(cfg, flags=_lib.FLAG_LANE_DENSE))
     assert torch.isfinite(h_reg).all() and h_reg.abs().max() > 0
     _close(h_reg.cpu(), h_ser.cpu(), FWD_RTOL, msg="register vs lane-serial")
