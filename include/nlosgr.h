@@ -142,6 +142,8 @@ typedef struct {
                                            instead of the register (lane = bin) kernel */
 #define NLOSGR_FLAG_BWD_SHARED   0x1000 /* backward: shared-row layout (4 waves per staged row) */
 #define NLOSGR_FLAG_BWD_PERWAVE  0x2000 /* backward: per-wave row layout (default picks by LDS size) */
+#define NLOSGR_FLAG_TILE_NOBIN   0x8000 /* ray-tile engine: cull every Gaussian against every item's cone in the
+                                           kernel instead of reading the tile bins (A/B: same selections) */
 #define NLOSGR_FLAG_FX_MAXUNIT   0x4000 /* forward FX drain: unit from the largest amplitude bound (the round-5
                                            rule, diagnostics: shows the precision the quantile unit recovers) */
 

@@ -119,6 +119,9 @@ struct TArgs {
                                 // static schedule, whose slot-private accumulator rows need a fixed order)
     float2* rcache;          // OCCL row cache [nitems][rt][nr] (D, W) (opt.ray_cache): the forward's rows,
                              // reloaded by the backward instead of re-running its first sweep
+    const float* cones;      // [P][ntiles][8] tile cones of this launch's wall points (tile_cone_kernel)
+    const unsigned long long* masks;   // tile bins [P][ntiles][nwords] (tile_bin_kernel), or null: cull in-kernel
+    int nwords;              // 64-Gaussian words per tile bin row
 };
 
 __host__ __device__ inline int tile_rays(int nr) {
@@ -238,6 +241,91 @@ __global__ __launch_bounds__(256) void cull_prep_kernel(nlosgr_gaussians g, cons
     cull[i] = make_float4(r.a.x, r.a.y, r.a.z, rad);
 }
 
+// Tile cull test: the sphere (c.xyz, radius c.w) against the tile's cone (axis a, half-angle h):
+// angle(v, a) <= h + asin(R / |v|)  <=>  v.a >= cos h sqrt(|v|^2 - R^2) - sin h R, v = mu - p.  No fp
+// contraction (explicit fmaf), so tile_bin_kernel and the in-kernel cull agree bit for bit.
+__device__ __forceinline__ bool cone_hit(float4 c, float px, float py, float pz, float ax, float ay, float az, float ch,
+                                         float shh, bool pass_all) {
+#pragma clang fp contract(off)
+    const float vx = c.x - px, vy = c.y - py, vz = c.z - pz;
+    const float d2 = fmaf(vz, vz, fmaf(vy, vy, vx * vx));
+    const float R2 = c.w * c.w;
+    if (pass_all || d2 <= R2 || !(c.w < INFINITY)) return true;
+    return fmaf(vz, az, fmaf(vy, ay, vx * ax)) >= fmaf(ch, sqrtf(d2 - R2), -(shh * c.w));
+}
+
+// Tile cones of one launch's items (wave = (wall point, tile), lane = ray of the tile): the mean ray
+// direction as axis, the largest ray angle to it + 2e-4 as half-angle (pass-all past 1.5 rad).
+// cones[(p * ntiles + t) * 8] = (ax, ay, az, cos h, sin h, pass_all, 0, 0).
+__global__ __launch_bounds__(256) void tile_cone_kernel(nlosgr_geometry geo, int ti, int tj, int ntile_j, int ntiles,
+                                                        float* cones) {
+    const long long item = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (item >= (long long)geo.nwall * ntiles) return;
+    const int lane = lane_id();
+    const int p = (int)(item / ntiles), t = (int)(item - (long long)p * ntiles);
+    const int nt = geo.nt, np_ = geo.np, rt = ti * tj;
+    const int ti0 = (t / ntile_j) * ti, tj0 = (t % ntile_j) * tj;
+    const int i = ti0 + lane / tj, j = tj0 + lane % tj;
+    const bool v = lane < rt && i < nt && j < np_;
+    float dx = 0.f, dy = 0.f, dz = 0.f;
+    if (v) {
+        const float st = geo.sin_theta[(size_t)p * nt + i];
+        dx = st * geo.cos_phi[(size_t)p * np_ + j];
+        dy = st * geo.sin_phi[(size_t)p * np_ + j];
+        dz = geo.cos_theta[(size_t)p * nt + i];
+    }
+    float sx = dx, sy = dy, sz = dz;
+    for (int off = 32; off > 0; off >>= 1) {
+        sx += __shfl_xor(sx, off); sy += __shfl_xor(sy, off); sz += __shfl_xor(sz, off);
+    }
+    const float n = sqrtf(sx * sx + sy * sy + sz * sz);
+    const float ax = n > 0.f ? sx / n : 0.f, ay = n > 0.f ? sy / n : 0.f, az = n > 0.f ? sz / n : 1.f;
+    float c = v ? fminf(1.0f, dx * ax + dy * ay + dz * az) : 1.0f;
+    for (int off = 32; off > 0; off >>= 1) c = fminf(c, __shfl_xor(c, off));
+    const float h = acosf(c) + 2e-4f;
+    if (lane == 0) {
+        float* o = cones + item * 8;
+        *reinterpret_cast<float4*>(o) = make_float4(ax, ay, az, cosf(h));
+        *reinterpret_cast<float4*>(o + 4) = make_float4(sinf(h), (h > 1.5f || n == 0.f) ? 1.f : 0.f, 0.f, 0.f);
+    }
+}
+
+// Tile binning (north_star's "tile binning"): for each wall point of the launch and each tile, one bit per
+// Gaussian: does its cull sphere pass the tile's cone (cone_hit, the in-kernel cull's test).  Workgroup =
+// (1024-Gaussian chunk, wall point), thread = Gaussian; per tile the wave's ballot is one 64-Gaussian word,
+// staged in LDS so each tile's 16 words of the chunk go out as one 128-B store.  Rows [p][t][nwords] keep
+// index order, so the tile kernel's queue (and path C's first-256-by-index rule) sees exactly the culled
+// sequence it would have built itself, without testing every Gaussian for every item.
+constexpr int kBinTB = 1024;
+__global__ __launch_bounds__(kBinTB) void tile_bin_kernel(const float4* __restrict__ cull, int ng, nlosgr_geometry geo,
+                                                          int ntiles, int nwords, const float* __restrict__ cones,
+                                                          unsigned long long* masks) {
+    __shared__ float cs[64 * 8];
+    __shared__ unsigned long long wb[64][kBinTB / 64];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = lane_id();
+    const int p = blockIdx.y;
+    const int g = blockIdx.x * kBinTB + tid;
+    const float4 c = g < ng ? cull[g] : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float px = geo.wall[3 * p], py = geo.wall[3 * p + 1], pz = geo.wall[3 * p + 2];
+    const float* cp = cones + (size_t)p * ntiles * 8;
+    for (int tb = 0; tb < ntiles; tb += 64) {
+        const int nb = min(64, ntiles - tb);
+        __syncthreads();
+        if (tid < nb * 8) cs[tid] = cp[(size_t)tb * 8 + tid];
+        __syncthreads();
+        for (int tt = 0; tt < nb; ++tt) {
+            const float* q = cs + tt * 8;
+            const bool hit = g < ng && cone_hit(c, px, py, pz, q[0], q[1], q[2], q[3], q[4], q[5] != 0.f);
+            const unsigned long long w = __builtin_amdgcn_ballot_w64(hit);
+            if (lane == 0) wb[tt][wave] = w;
+        }
+        __syncthreads();
+        const int tt = tid / (kBinTB / 64), wv = tid % (kBinTB / 64);
+        const int word = blockIdx.x * (kBinTB / 64) + wv;
+        if (tt < nb && word < nwords) masks[((size_t)p * ntiles + tb + tt) * nwords + word] = wb[tt][wv];
+    }
+}
+
 // ------------------------------------------------------------------------------------------
 // the tile kernel (forward: BWD = false; backward: BWD = true)
 // ------------------------------------------------------------------------------------------
@@ -256,8 +344,8 @@ __global__ __launch_bounds__(tile_threads<BWD>()) void tile_kernel(TArgs k) {
     int* icnt = reinterpret_cast<int*>(misc);          // [64] AABB cap counters per ray
     int* ihalf = icnt + 64;                             // [64] per-window hits of the first staged half
     constexpr int kCullU = cull_u<BWD>();
-    int* iwave = icnt + 128;                            // [kCullU][16] cull counts per wave (<= 64 ints)
-    float* cone = misc + 160;                           // axis xyz, cos h, sin h, pass-all flag
+    int* iwave = icnt + 128;                            // [kCullU][kTW] cull counts per wave / bin-round scan (64 ints)
+    static_assert(cull_u<BWD>() * kTW <= 64 && 3 * kTW <= 64, "per-wave cull counts overflow misc[128, 192)");
     const int tid = threadIdx.x, wave = tid >> 6, lane = lane_id();
     const int RT = k.rt;
     // AABB selection: each selected Gaussian over the samples within the cutoff (5.7 sigma = parity
@@ -308,32 +396,16 @@ __global__ __launch_bounds__(tile_threads<BWD>()) void tile_kernel(TArgs k) {
         const float* sph = k.geo.sin_phi + (size_t)p * np_;
         const float* cph = k.geo.cos_phi + (size_t)p * np_;
         __syncthreads();   // previous item done with LDS
-        // tile cone (wave 0, lane = ray of the tile)
-        if (wave == 0) {
-            const int i = ti0 + lane / k.tj, j = tj0 + lane % k.tj;
-            const bool v = lane < RT && i < nt && j < np_;
-            float dx = 0.f, dy = 0.f, dz = 0.f;
-            if (v) { dx = sth[i] * cph[j]; dy = sth[i] * sph[j]; dz = cth[i]; }
-            float sx = dx, sy = dy, sz = dz;
-            for (int off = 32; off > 0; off >>= 1) {
-                sx += __shfl_xor(sx, off); sy += __shfl_xor(sy, off); sz += __shfl_xor(sz, off);
-            }
-            const float n = sqrtf(sx * sx + sy * sy + sz * sz);
-            const float ax = n > 0.f ? sx / n : 0.f, ay = n > 0.f ? sy / n : 0.f, az = n > 0.f ? sz / n : 1.f;
-            float c = v ? fminf(1.0f, dx * ax + dy * ay + dz * az) : 1.0f;
-            for (int off = 32; off > 0; off >>= 1) c = fminf(c, __shfl_xor(c, off));
-            const float h = acosf(c) + 2e-4f;
-            if (lane == 0) {
-                cone[0] = ax; cone[1] = ay; cone[2] = az;
-                cone[3] = cosf(h); cone[4] = sinf(h);
-                cone[5] = (h > 1.5f || n == 0.f) ? 1.f : 0.f;
-            }
-            if (lane < 64) icnt[lane] = 0;
-        }
+        if (tid < 64) icnt[tid] = 0;
         for (int x = tid; x < RT * nr; x += kTB) rows[x] = make_float2(0.f, 0.f);
         __syncthreads();
-        const float ax = cone[0], ay = cone[1], az = cone[2], ch = cone[3], shh = cone[4];
-        const bool pass_all = cone[5] != 0.f;
+        // the tile's cone from the table (tile_cone_kernel: the same values the bins were built with)
+        const float* cn = k.cones + ((size_t)p * k.ntiles + t) * 8;
+        const float4 cA = *reinterpret_cast<const float4*>(cn), cB = *reinterpret_cast<const float4*>(cn + 4);
+        const float ax = cA.x, ay = cA.y, az = cA.z, ch = cA.w, shh = cB.x;
+        const bool pass_all = cB.y != 0.f;
+        // tile bins: this item's row of 64-Gaussian hit words (index order)
+        const unsigned long long* mrow = k.masks ? k.masks + ((size_t)p * k.ntiles + t) * k.nwords : nullptr;
 
         // ---------------- sweeps over the Gaussians (forward: 1; backward: 2) ----------------
         for (int sweep = 0; sweep < (BWD ? 2 : 1); ++sweep) {
@@ -359,11 +431,12 @@ __global__ __launch_bounds__(tile_threads<BWD>()) void tile_kernel(TArgs k) {
 #pragma unroll
             for (int u = 0; u < kCullU; ++u) {
                 cnext[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-                if (!skip0 && u * kTB + tid < k.g.ng) cnext[u] = k.cull[u * kTB + tid];
+                if (!skip0 && !mrow && u * kTB + tid < k.g.ng) cnext[u] = k.cull[u * kTB + tid];
             }
-            for (int g0 = 0; !skip0 && !capped && (g0 < k.g.ng || qn > qh); g0 += kCullU * kTB) {
-                // ---- cull round: lane = Gaussian, kCullU x kTB per round, ordered append ----
-                if (g0 < k.g.ng) {
+            // g0: the next Gaussian (in-kernel cull) or the next 64-Gaussian word of the item's bin row
+            const int gend = mrow ? k.nwords : k.g.ng;
+            for (int g0 = 0; !skip0 && !capped && (g0 < gend || qn > qh);) {
+                if (g0 < gend) {
                     if (qh > 0) {
                         // what the windows left (< kWin entries) moves to the front once per cull round
                         const int rest = qn - qh;
@@ -374,6 +447,52 @@ __global__ __launch_bounds__(tile_threads<BWD>()) void tile_kernel(TArgs k) {
                         qn = rest;
                         qh = 0;
                     }
+                    if (mrow) {
+                        // ---- bin round: thread = one 64-Gaussian word; the words whose hits fit the queue
+                        // (kCullU x kTB entries; a prefix of the threads) append their indices in order ----
+                        constexpr int cap = kCullU * kTB;
+                        const int wi = g0 + tid;
+                        const unsigned long long wd = wi < gend ? mrow[wi] : 0ull;
+                        const int h = __popcll(wd);
+                        int incl = h;
+#pragma unroll
+                        for (int off = 1; off < 64; off <<= 1) {
+                            const int u = __shfl_up(incl, off);
+                            if (lane >= off) incl += u;
+                        }
+                        if (lane == 63) iwave[wave] = incl;
+                        __syncthreads();
+                        int base = 0;
+#pragma unroll
+                        for (int w = 0; w < kTW; ++w) base += w < wave ? iwave[w] : 0;
+                        const int ex = base + incl - h;
+                        const bool take = wi < gend && ex + h <= cap;
+                        if (take) {
+                            unsigned long long m = wd;
+                            int o = qn + ex;
+                            while (m) {
+                                queue[o++] = wi * 64 + (int)__builtin_ctzll(m);
+                                m &= m - 1ull;
+                            }
+                        }
+                        const int wtake = __popcll(__builtin_amdgcn_ballot_w64(take));
+                        const int went = wave_max_i(take ? ex + h : 0);
+                        if (lane == 0) {
+                            iwave[kTW + wave] = wtake;
+                            iwave[2 * kTW + wave] = went;
+                        }
+                        __syncthreads();
+                        int nw = 0, ne = 0;
+#pragma unroll
+                        for (int w = 0; w < kTW; ++w) {
+                            nw += iwave[kTW + w];
+                            ne = max(ne, iwave[2 * kTW + w]);
+                        }
+                        g0 += nw;
+                        qn += ne;
+                        __syncthreads();   // (iwave is rewritten by the next round)
+                        TDIAG(tcull)
+                    } else {
                     bool hit[kCullU];
                     unsigned long long m[kCullU];
 #pragma unroll
@@ -381,18 +500,7 @@ __global__ __launch_bounds__(tile_threads<BWD>()) void tile_kernel(TArgs k) {
                         const int gi = g0 + u * kTB + tid;
                         const float4 c = cnext[u];
                         if (gi + kCullU * kTB < k.g.ng) cnext[u] = k.cull[gi + kCullU * kTB];
-                        hit[u] = false;
-                        if (gi < k.g.ng) {
-                            const float vx = c.x - px, vy = c.y - py, vz = c.z - pz;
-                            const float d2 = vx * vx + vy * vy + vz * vz;
-                            const float R2 = c.w * c.w;
-                            if (pass_all || d2 <= R2 || !(c.w < INFINITY)) {
-                                hit[u] = true;
-                            } else {
-                                // angle(v, axis) <= h + asin(R / |v|)  <=>  v.a >= cos h sqrt(|v|^2 - R^2) - sin h R
-                                hit[u] = vx * ax + vy * ay + vz * az >= ch * sqrtf(d2 - R2) - shh * c.w;
-                            }
-                        }
+                        hit[u] = gi < k.g.ng && cone_hit(c, px, py, pz, ax, ay, az, ch, shh, pass_all);
                         m[u] = __builtin_amdgcn_ballot_w64(hit[u]);
                         if (lane == 0) iwave[u * kTW + wave] = __popcll(m[u]);
                     }
@@ -419,8 +527,10 @@ __global__ __launch_bounds__(tile_threads<BWD>()) void tile_kernel(TArgs k) {
                     qn = run;
                     __syncthreads();
                     TDIAG(tcull)
+                    g0 += kCullU * kTB;
+                    }
                 }
-                const bool last = g0 + kCullU * kTB >= k.g.ng;
+                const bool last = g0 >= gend;
                 // ---- windows of up to 128 staged Gaussians ----
                 while (qn - qh >= kWin || (last && qn > qh)) {
                     const int nst = min(qn - qh, kWin);
@@ -1062,9 +1172,16 @@ int cu_count() {
 struct TPlan {
     int rt, ti, tj, nti, ntj, ntiles, nslot;
     int pbatch;              // forward: wall points per launch (the tile partials [pbatch][ntiles][nr] stay bounded)
+    int bbatch;              // wall points per launch of either sweep (the tile bins [bbatch][ntiles][nwords] too)
+    int nwords;              // 64-Gaussian words per tile bin row
+    bool bins;               // tile binning on (culled selections; NLOSGR_FLAG_TILE_NOBIN turns it off)
     long long nitems;
-    size_t off_cull, off_bbox, off_acc, off_hpart, off_next, off_rows, total;
+    size_t off_cull, off_bbox, off_acc, off_hpart, off_next, off_cones, off_masks, off_rows, total;
 };
+
+// tile bins per launch: at most this many bytes (C3: 64 tiles x 1563 words = 800 KB per wall point, so
+// 4096-wall-point launches use 3.3 GB; C5's 500k Gaussians x 128 tiles: 524 wall points per launch)
+constexpr size_t kBinBytes = (size_t)4 << 30;
 
 // the OCCL row cache: 8 B per (item, tile ray, bin), e.g. C3 (128x128 wall, 32x32 rays, 1024 bins) 128 GiB
 bool row_cache(const nlosgr_options* opt) { return opt && opt->ray_cache && opt->mode == NLOSGR_MODE_OCCL; }
@@ -1096,7 +1213,21 @@ TPlan plan(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_o
     P.pbatch = (int)(pb < geo->nwall ? pb : geo->nwall);
     if (P.pbatch < 1) P.pbatch = 1;
     P.off_next = P.off_hpart + align_up((size_t)P.pbatch * per_wall);
-    P.off_rows = P.off_next + align_up(sizeof(unsigned long long));
+    // tile binning: every culled selection (AABB boxes, or the support within a cutoff); with a dense support
+    // every Gaussian passes every cone, so there is nothing to bin
+    P.bins = !(opt->flags & NLOSGR_FLAG_TILE_NOBIN) &&
+             (opt->selection == NLOSGR_SELECT_AABB || opt->cutoff > 0.f) && g->ng > 0;
+    P.nwords = (int)((ng + 63) / 64);
+    const size_t per_wall_bins = P.bins ? (size_t)P.ntiles * P.nwords * sizeof(unsigned long long) : 0;
+    long long bb = per_wall_bins ? (long long)(kBinBytes / per_wall_bins) : geo->nwall;
+    if (bb < 1) bb = 1;
+    P.bbatch = (int)(bb < geo->nwall ? bb : geo->nwall);
+    if (P.bbatch < 1) P.bbatch = 1;
+    // the launches of both sweeps cover the same wall-point batches (the forward's partials bound it too)
+    if (P.pbatch > P.bbatch) P.pbatch = P.bbatch;
+    P.off_cones = P.off_next + align_up(sizeof(unsigned long long));
+    P.off_masks = P.off_cones + align_up((size_t)P.bbatch * P.ntiles * 8 * sizeof(float));
+    P.off_rows = P.off_masks + align_up((size_t)P.bbatch * per_wall_bins);
     P.total = P.off_rows + (row_cache(opt) ? align_up((size_t)P.nitems * P.rt * geo->nr * sizeof(float2)) : 0);
     return P;
 }
@@ -1159,6 +1290,9 @@ int prepare(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_
     a.nitems = P.nitems; a.nslot = P.nslot;
     a.rcache = row_cache(opt) ? (float2*)(base + P.off_rows) : nullptr;
     a.next = (unsigned long long*)(base + P.off_next);
+    a.cones = (const float*)(base + P.off_cones);
+    a.masks = P.bins ? (const unsigned long long*)(base + P.off_masks) : nullptr;
+    a.nwords = P.nwords;
     launch_preprocess(g, (GaussRec*)base, s);
     HIPCHK(hipGetLastError());
     const int nb = (g->ng + 255) / 256;
@@ -1169,6 +1303,40 @@ int prepare(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_
         hipLaunchKernelGGL(cull_prep_kernel<NLOSGR_SELECT_SUPPORT>, dim3(nb), dim3(256), 0, s, *g, a.recs, opt->cutoff,
                            (float4*)a.cull, (float*)a.bbox);
     HIPCHK(hipGetLastError());
+    return NLOSGR_OK;
+}
+
+// the launch arguments of wall points [p0, p0 + pn): geometry tables, the row cache and the items offset
+TArgs batch_args(const TArgs& a, const TPlan& P, const nlosgr_geometry* geo, int p0, int pn) {
+    const int nt = geo->nt, np_ = geo->np, nr = geo->nr;
+    TArgs b = a;
+    b.geo.nwall = pn;
+    b.geo.wall = geo->wall + 3 * (size_t)p0;
+    b.geo.sin_theta = geo->sin_theta + (size_t)p0 * nt;
+    b.geo.cos_theta = geo->cos_theta + (size_t)p0 * nt;
+    b.geo.sin_phi = geo->sin_phi + (size_t)p0 * np_;
+    b.geo.cos_phi = geo->cos_phi + (size_t)p0 * np_;
+    b.geo.grid_lin = geo->grid_lin + 4 * (size_t)p0;
+    b.geo.hscale = geo->hscale + p0;
+    b.nitems = (long long)pn * P.ntiles;
+    b.pbase = p0;   // the tile rotation follows the global wall index
+    b.nslot = (int)(b.nitems < P.nslot ? b.nitems : P.nslot);
+    b.rcache = a.rcache ? a.rcache + (size_t)p0 * P.ntiles * P.rt * nr : nullptr;
+    return b;
+}
+
+// the batch's tile cones, and its tile bins when binning is on
+int bin_batch(const TArgs& b, const TPlan& P, hipStream_t s) {
+    const long long nthr = b.nitems * 64;
+    hipLaunchKernelGGL(tile_cone_kernel, dim3((unsigned)((nthr + 255) / 256)), dim3(256), 0, s, b.geo, P.ti, P.tj,
+                       P.ntj, P.ntiles, (float*)b.cones);
+    HIPCHK(hipGetLastError());
+    if (b.masks) {
+        hipLaunchKernelGGL(tile_bin_kernel, dim3((unsigned)((b.g.ng + kBinTB - 1) / kBinTB), (unsigned)b.geo.nwall),
+                           dim3(kBinTB), 0, s, b.cull, b.g.ng, b.geo, P.ntiles, P.nwords, b.cones,
+                           (unsigned long long*)b.masks);
+        HIPCHK(hipGetLastError());
+    }
     return NLOSGR_OK;
 }
 
@@ -1189,7 +1357,8 @@ int tiles_validate(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const 
     if (opt->selection != NLOSGR_SELECT_SUPPORT && opt->selection != NLOSGR_SELECT_AABB)
         return set_err(NLOSGR_E_INVALID, "unknown selection");
     if (geo->nr > 4096) return set_err(NLOSGR_E_UNSUPPORTED, "occl / AABB engine: nr <= 4096");
-    if ((size_t)TLayout(tile_rays(geo->nr), geo->nr, tile_threads<false>(), false).total * 4 + 16 > 160 * 1024)
+    if ((size_t)TLayout(tile_rays(geo->nr), geo->nr, tile_threads<false>(), false).total * 4 + 16 > 160 * 1024 ||
+        (size_t)TLayout(tile_rays(geo->nr), geo->nr, tile_threads<true>(), true).total * 4 + 16 > 160 * 1024)
         return set_err(NLOSGR_E_UNSUPPORTED, "occl / AABB engine: LDS budget");
     return NLOSGR_OK;
 }
@@ -1212,27 +1381,16 @@ int tiles_fwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosg
     if (rc) return rc;
     const size_t shm = (size_t)TLayout(P.rt, geo->nr, tile_threads<false>(), false).total * sizeof(float);
     const int nt = geo->nt, np_ = geo->np, nr = geo->nr;
-    float2* rc0 = a.rcache;
     // wall-point batches: one launch each over the batch's items (pointer offsets into the tables, the
-    // outputs and the row cache), so the tile partials stay within kHpartBytes
+    // outputs and the row cache), so the tile partials and the tile bins stay within their budgets
     for (int p0 = 0; p0 < geo->nwall; p0 += P.pbatch) {
         const int pn = geo->nwall - p0 < P.pbatch ? geo->nwall - p0 : P.pbatch;
-        TArgs b = a;
-        b.geo.nwall = pn;
-        b.geo.wall = geo->wall + 3 * (size_t)p0;
-        b.geo.sin_theta = geo->sin_theta + (size_t)p0 * nt;
-        b.geo.cos_theta = geo->cos_theta + (size_t)p0 * nt;
-        b.geo.sin_phi = geo->sin_phi + (size_t)p0 * np_;
-        b.geo.cos_phi = geo->cos_phi + (size_t)p0 * np_;
-        b.geo.grid_lin = geo->grid_lin + 4 * (size_t)p0;
-        b.geo.hscale = geo->hscale + p0;
-        b.nitems = (long long)pn * P.ntiles;
-        b.pbase = p0;   // the tile rotation follows the global wall index (the backward's row-cache items)
-        b.nslot = (int)(b.nitems < P.nslot ? b.nitems : P.nslot);
+        TArgs b = batch_args(a, P, geo, p0, pn);
         b.hist_out = hist_out;
         b.ray_out = ray_out ? ray_out + (size_t)p0 * nt * np_ * nr : nullptr;
-        b.rcache = rc0 ? rc0 + (size_t)p0 * P.ntiles * P.rt * nr : nullptr;
         HIPCHK(hipMemsetAsync(b.next, 0, sizeof(unsigned long long), s));
+        rc = bin_batch(b, P, s);
+        if (rc) return rc;
         dispatch_tile<false>(b, shm, s);
         HIPCHK(hipGetLastError());
         if (hist_out) {
@@ -1258,8 +1416,19 @@ int tiles_bwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosg
     HIPCHK(hipMemsetAsync(a.acc, 0, (size_t)P.nslot * g->ng * kRec * sizeof(float), s));
     if (geo->nwall > 0 && (grad_hist || grad_ray)) {
         const size_t shm = (size_t)TLayout(P.rt, geo->nr, tile_threads<true>(), true).total * sizeof(float);
-        dispatch_tile<true>(a, shm, s);
-        HIPCHK(hipGetLastError());
+        const int nt = geo->nt, np_ = geo->np, nr = geo->nr;
+        // the forward's wall-point batches (the row cache's items and the bins' budget); every launch adds into
+        // the same slot rows, in batch order
+        for (int p0 = 0; p0 < geo->nwall; p0 += P.pbatch) {
+            const int pn = geo->nwall - p0 < P.pbatch ? geo->nwall - p0 : P.pbatch;
+            TArgs b = batch_args(a, P, geo, p0, pn);
+            b.grad_hist = grad_hist ? grad_hist + (size_t)p0 * nr : nullptr;
+            b.grad_ray = grad_ray ? grad_ray + (size_t)p0 * nt * np_ * nr : nullptr;
+            rc = bin_batch(b, P, s);
+            if (rc) return rc;
+            dispatch_tile<true>(b, shm, s);
+            HIPCHK(hipGetLastError());
+        }
     }
     hipLaunchKernelGGL(tiles_finish_kernel, dim3((g->ng + 255) / 256), dim3(256), 0, s, a, d_mu, d_scaling, d_rotation,
                        d_opacity, d_features);

@@ -69,6 +69,7 @@ FLAG_LANE_DENSE = 0x800    # dense no-occlusion histogram through the lane-seria
 FLAG_BWD_SHARED = 0x1000   # backward: shared-row layout
 FLAG_BWD_PERWAVE = 0x2000  # backward: per-wave row layout
 FLAG_FX_MAXUNIT = 0x4000   # FX drain unit from the largest bound (round-5 rule; diagnostics)
+FLAG_TILE_NOBIN = 0x8000   # ray-tile engine: in-kernel cull instead of the tile bins (A/B)
 
 # every symbol include/nlosgr.h declares (tests check the exports against this list)
 EXPORTS = ["nlosgr_workspace_bytes", "nlosgr_render_fwd", "nlosgr_render_bwd", "nlosgr_count_support", "nlosgr_fx_info",
