@@ -141,13 +141,16 @@ def committed_profile(cfg_name, kind, cutoff, preset="cuda", mode="noocl", selec
 # the kernels each timed phase launches (families: the kernel's name without template arguments);
 # preprocess_kernel runs once in each phase
 PHASE_KERNELS = {
-    "fwd": ("preprocess_kernel", "fx_amax_kernel", "fwd_kernel", "fwd_dense_kernel", "fx_reduce_kernel",
-            "hist_reduce_kernel"),
+    "fwd": ("preprocess_kernel", "fx_bound_kernel", "fx_unit_kernel", "fwd_kernel", "fwd_dense_kernel",
+            "fx_reduce_kernel", "hist_reduce_kernel"),
     "bwd": ("preprocess_kernel", "bwd_kernel", "sh_kernel", "finish_kernel"),
-    "tiles_fwd": ("preprocess_kernel", "tile_kernel", "tiles_reduce_kernel"),
-    "tiles_bwd": ("preprocess_kernel", "tile_kernel", "tiles_finish_kernel"),
+    "tiles_fwd": ("preprocess_kernel", "cull_prep_kernel", "tile_cone_kernel", "tile_bin_kernel", "tile_kernel",
+                  "tiles_reduce_kernel"),
+    "tiles_bwd": ("preprocess_kernel", "cull_prep_kernel", "tile_cone_kernel", "tile_bin_kernel", "tile_kernel",
+                  "tiles_finish_kernel"),
 }
-SHARED_KERNELS = ("preprocess_kernel",)
+# kernels both phases launch (the same names in the profile): half their launches per step count per phase
+SHARED_KERNELS = ("preprocess_kernel", "cull_prep_kernel", "tile_cone_kernel", "tile_bin_kernel")
 
 
 def kernel_family(name):
@@ -156,22 +159,29 @@ def kernel_family(name):
     return n.split("<", 1)[0].strip()
 
 
+def rec_has_count(kernels):
+    return any(kernel_family(k) == "count_kernel" for k in kernels)
+
+
 def phase_traffic(kernels, phase):
     """HBM bytes per step of one timed phase from a traffic profile's per-kernel records: every kernel
-    of the phase's families that runs every step (launches_per_step >= 0.5: the untimed support-count
-    launch runs once per run and is left out), each at its launches per step (a kernel of both phases
-    counts one launch per phase); the ray-tile engine's tile_kernel<SEL, DENSE, OCCL, BWD> is split by
-    its BWD argument.  Returns (bytes, [kernel names]) or (None, [])."""
+    of the phase's families (the untimed support count runs as count_kernel, a family of its own, so it
+    is left out by name whatever the profile's step count), each at its launches per step (a kernel of
+    both phases counts half of them per phase); the ray-tile engine's tile_kernel<SEL, DENSE, OCCL, BWD>
+    is split by its BWD argument.  Returns (bytes, [kernel names]) or (None, [])."""
     fams = PHASE_KERNELS[phase]
     total, used = 0.0, []
     for k, v in kernels.items():
         fam = kernel_family(k)
-        if fam not in fams or v.get("launches_per_step", 1.0) < 0.5:
+        if fam not in fams:
             continue
+        if fam == "fwd_kernel" and v.get("launches_per_step", 1.0) < 0.5 and not rec_has_count(kernels):
+            continue   # profiles older than count_kernel: the support count was a once-per-run fwd_kernel
         if fam == "tile_kernel" and k.rstrip().endswith("true>") != (phase == "tiles_bwd"):
             continue
         per = v["hbm_bytes_per_launch"]
-        total += per if fam in SHARED_KERNELS else per * v.get("launches_per_step", 1.0)
+        lps = v.get("launches_per_step", 1.0)
+        total += per * (0.5 * lps if fam in SHARED_KERNELS else lps)
         used.append(k)
     return (total, used) if used else (None, [])
 

@@ -145,25 +145,13 @@ __device__ __forceinline__ void gauss_bbox(const nlosgr_gaussians& g, int i, flo
     }
 }
 
-// dL/dA (acc[0..8], A = diag(1/s~) R') -> dL/d_scaling, dL/d_rotation of Gaussian i under the preset
+// dL/dR' (dRp[9]) and dL/ds~ (dst[3]) -> dL/d_scaling, dL/d_rotation of Gaussian i under the preset
 template <int PRESET>
-__device__ void chain_to_raw(const nlosgr_gaussians& g, int i, const float* acc, float* d_scaling, float* d_rot) {
+__device__ void chain_core(const nlosgr_gaussians& g, int i, const GaussAct& a, const float* dRp, const float* dst,
+                           float* d_scaling, float* d_rot) {
     const float* S = g.scaling + 3 * i;
     const float* Q = g.rotation + 4 * i;
-    const float O = g.opacity[i];
     const float mod = g.scaling_modifier;
-    GaussAct a;
-    activate<PRESET>(S, Q, O, mod, a);
-    // A_rc = R'_rc / s~_r
-    float dRp[9], dst[3];
-    for (int r = 0; r < 3; ++r) {
-        float acc_s = 0.f;
-        for (int c = 0; c < 3; ++c) {
-            dRp[3 * r + c] = acc[3 * r + c] / a.st[r];
-            acc_s += acc[3 * r + c] * a.Rp[3 * r + c];
-        }
-        dst[r] = -acc_s / (a.st[r] * a.st[r]);
-    }
     float dR[9];
     if (PRESET == NLOSGR_PRESET_TORCH) {
         for (int t = 0; t < 9; ++t) dR[t] = dRp[t];
@@ -204,6 +192,77 @@ __device__ void chain_to_raw(const nlosgr_gaussians& g, int i, const float* acc,
             for (int t = 0; t < 4; ++t) d_rot[4 * i + t] = (dqn[t] - qn[t] * dp) / n;
         }
     }
+}
+
+// dL/dA (acc[0..8], A = diag(1/s~) R') -> dL/d_scaling, dL/d_rotation of Gaussian i under the preset
+template <int PRESET>
+__device__ void chain_to_raw(const nlosgr_gaussians& g, int i, const float* acc, float* d_scaling, float* d_rot) {
+    GaussAct a;
+    activate<PRESET>(g.scaling + 3 * i, g.rotation + 4 * i, g.opacity[i], g.scaling_modifier, a);
+    // A_rc = R'_rc / s~_r
+    float dRp[9], dst[3];
+    for (int r = 0; r < 3; ++r) {
+        float acc_s = 0.f;
+        for (int c = 0; c < 3; ++c) {
+            dRp[3 * r + c] = acc[3 * r + c] / a.st[r];
+            acc_s += acc[3 * r + c] * a.Rp[3 * r + c];
+        }
+        dst[r] = -acc_s / (a.st[r] * a.st[r]);
+    }
+    chain_core<PRESET>(g, i, a, dRp, dst, d_scaling, d_rot);
+}
+
+// Scale ratios of A = diag(1/s~) R' from its row norms (|A_r| = 1/s~_r): r2 = s~2^2/s~1^2, r3 = s~3^2/s~1^2.
+// No contraction, so the backward kernel and the finish compute the same ratios.
+__device__ __forceinline__ void scale_ratios(const float* A, float& r2, float& r3) {
+#pragma clang fp contract(off)
+    const float n1 = A[0] * A[0] + A[1] * A[1] + A[2] * A[2];
+    const float n2 = A[3] * A[3] + A[4] * A[4] + A[5] * A[5];
+    const float n3 = A[6] * A[6] + A[7] * A[7] + A[8] * A[8];
+    r2 = n1 / n2;
+    r3 = n1 / n3;
+}
+
+// The backward's shape accumulators (round 6).  A contribution to dL/dA is an outer product g b^T (g = dL/du0
+// with b = p - mu, or g = dL/dv with b = the ray direction); in whitened form M = dA A^T = g w^T, w = A b.
+// Only 6 of its 9 degrees of freedom reach the raw parameters: the diagonal D_r = g_r w_r (the scales:
+// dL/ds~_r = -D_r / s~_r) and the antisymmetric part of Omega = dR' R'^T = S~^-1 M S~ (the rotation),
+// accumulated per contribution as K~ = s~1^2 (Omega - Omega^T)_ij / (s~i s~j) ... scaled so only the ratios
+// r = s~^2 / s~1^2 appear:  K~23 = r3 g2 w3 - r2 g3 w2,  K~31 = g3 w1 - r3 g1 w3,  K~12 = r2 g1 w2 - g2 w1.
+// Summing dA itself (round 5) carried the large symmetric part into every add, so the small rotational part
+// came out of a cancellation (TrainStep's ordered vs unordered backward differed by 3.6e-5 of max in
+// d_rotation against 1.8e-7 elsewhere); the rotational sums here never hold the symmetric part.
+__device__ __forceinline__ void shape_acc(const float* gv, const float* w, float r2, float r3, float* D, float* K) {
+    D[0] = fmaf(gv[0], w[0], D[0]);
+    D[1] = fmaf(gv[1], w[1], D[1]);
+    D[2] = fmaf(gv[2], w[2], D[2]);
+    K[0] += r3 * gv[1] * w[2] - r2 * gv[2] * w[1];
+    K[1] += gv[2] * w[0] - r3 * gv[0] * w[2];
+    K[2] += r2 * gv[0] * w[1] - gv[1] * w[0];
+}
+
+// (D[3], K~[3]) of shape_acc -> dL/d_scaling, dL/d_rotation: dL/ds~_r = -D_r / s~_r; dL/dR' = Omega_a R' with
+// Omega_a = (Omega - Omega^T) / 2, (Omega - Omega^T)_ij = K~_ij / sqrt(r_i r_j) (its symmetric part never
+// reaches the rotation: the quaternion's tangent space sees only the antisymmetric part of dR' R'^T)
+template <int PRESET>
+__device__ void chain_to_raw_shape(const nlosgr_gaussians& g, int i, const float* D, const float* K, float* d_scaling,
+                                   float* d_rot) {
+    GaussAct a;
+    activate<PRESET>(g.scaling + 3 * i, g.rotation + 4 * i, g.opacity[i], g.scaling_modifier, a);
+    float A[9];
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) A[3 * r + c] = a.Rp[3 * r + c] / a.st[r];
+    float r2, r3;
+    scale_ratios(A, r2, r3);
+    float dst[3];
+    for (int r = 0; r < 3; ++r) dst[r] = -D[r] / a.st[r];
+    const float w23 = 0.5f * K[0] / sqrtf(r2 * r3), w31 = 0.5f * K[1] / sqrtf(r3), w12 = 0.5f * K[2] / sqrtf(r2);
+    const float Om[9] = {0.f, w12, -w31, -w12, 0.f, w23, w31, -w23, 0.f};
+    float dRp[9];
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c)
+            dRp[3 * r + c] = Om[3 * r] * a.Rp[c] + Om[3 * r + 1] * a.Rp[3 + c] + Om[3 * r + 2] * a.Rp[6 + c];
+    chain_core<PRESET>(g, i, a, dRp, dst, d_scaling, d_rot);
 }
 
 // ray-tile engine (nlosgr_tiles.hip): NLOSGR_MODE_OCCL and NLOSGR_SELECT_AABB

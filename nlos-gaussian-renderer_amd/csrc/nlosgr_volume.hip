@@ -585,8 +585,8 @@ __device__ __forceinline__ void fx_place(bool newl, bool act, Drain& d) {
     }
 }
 
-template <int PRESET, int MODE, bool DENSE, bool RAYS, bool CACHE, bool TAIL = false, bool FX = false>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) void fwd_kernel(KArgs k) {
+template <int PRESET, int MODE, bool DENSE, bool RAYS, bool CACHE, bool TAIL, bool FX>
+__device__ __forceinline__ void fwd_body(const KArgs& k) {
     extern __shared__ __align__(16) float smem[];
     const int nr = k.geo.nr, nt = k.geo.nt, np_ = k.geo.np;
     const FwdLayout L(nr, nt, np_, FX);
@@ -629,6 +629,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
     float fthr = kFxLimit / 64.f;   // wave-uniform
     float fpk = 0.f, fxs = 0.f;     // this lane's segment peak, and its peaks since the last check
     bool brt = false;               // FX: this lane's segment is bright (global u64 adds, see kFxBits)
+    bool wbright = false;           // FX, wave-uniform: some lane took a bright segment at the last refill (the
+                                    // set of bright active lanes only shrinks until the next refill)
     unsigned long long* const grow = FX ? k.hfx + (size_t)p * nr : nullptr;
     unsigned* hist32 = reinterpret_cast<unsigned*>(hist);
     const int nfx = nr + kSteps + 2;   // fields a round can reach (bins past nr are pad)
@@ -722,6 +724,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
                 if (FX) {
                     const unsigned long long bm = __builtin_amdgcn_ballot_w64(take && act && brt);
                     if (bm && lane == 0) atomicAdd(k.fx_info + 3, (int)__popcll(bm));
+                    wbright = __builtin_amdgcn_ballot_w64(act && brt) != 0ull;
                 }
                 const int ntake = min(nidle, qcount);
                 qhead = (qhead + ntake) & (kRQ - 1);
@@ -788,7 +791,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
                 const int lim = remw + o;   // slot j is in the segment iff o <= j < lim
                 // FX: bright lanes (brt) add into the wall point's global u64 row instead of the LDS; the
                 // rounds without one (all of them unless the bounds spread, see kFxBits) run the plain loop
-                const bool anyb = FX && __builtin_amdgcn_ballot_w64(win && brt) != 0ull;
+                const bool anyb = FX && wbright;
                 const int gb0 = d.pos & ~(VW - 1);
                 auto emit_l = [&](int kv, float v0, float v1) { emit2<FX>(reinterpret_cast<float2*>(hb) + kv, v0, v1); };
                 auto emit_g = [&](int kv, float v0, float v1) {
@@ -1060,6 +1063,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
     }
 }
 
+template <int PRESET, int MODE, bool DENSE, bool RAYS, bool CACHE, bool TAIL = false, bool FX = false>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) void fwd_kernel(KArgs k) {
+    fwd_body<PRESET, MODE, DENSE, RAYS, CACHE, TAIL, FX>(k);
+}
+// nlosgr_count_support's launch of the same body under its own name, so profiles tell it apart from the
+// timed forward by identity
+template <int PRESET, int MODE, bool DENSE, bool TAIL>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) void count_kernel(KArgs k) {
+    fwd_body<PRESET, MODE, DENSE, false, false, TAIL, false>(k);
+}
+
 // forward Gaussian splits: hist[p,t] = (sum over splits in order) x att[t] x hscale[p]
 __global__ __launch_bounds__(kBlock) void hist_reduce_kernel(const float* __restrict__ hpart, int nsp, long long P,
                                                              int nr, const float* __restrict__ att,
@@ -1329,7 +1343,8 @@ constexpr int kBSteps = NLOSGR_BSTEPS;   // bins per lane per backward drain rou
 // the staged gradient row is zero-padded by the longest round (no-occlusion TAIL rounds)
 constexpr int kmax_i(int a, int b) { return a > b ? a : b; }
 constexpr int kBPad = kmax_i(kmax_i(NLOSGR_BSTEPS_TAIL, kBSteps), kmax_i(NLOSGR_BSTEPS_NETF_TAIL, NLOSGR_BSTEPS_TAIL_SHR));
-constexpr int kBwdSlots = 13;   // per-Gaussian backward partial: dA[9], dMu[3], dsigma (stride 32 in HBM)
+constexpr int kBwdSlots = 13;   // per-Gaussian backward partial: D[3], K~[3], 0[3] (shape_acc), dMu[3], dsigma
+                                // (stride 32 in HBM)
 constexpr int kShPart = 28;     // sh_kernel partial: dF[KM <= 25], dMu[3] (at KM), pad
 
 // Two layouts.  Per-wave rows (default): each wave walks its own wall points and stages its own
@@ -1359,7 +1374,7 @@ struct BwdLayout {
         tth = al4(nr + kBPad);               // float2 [nt]
         tph = tth + al4(2 * nt);             // float2 [np]
         rayq = tph + al4(2 * np_);           // uint [kRQ] ring
-        pdat = rayq + kRQ;                   // pair table, 4 planes [4][64] float4: A[0:4] | A[4:8] | A[8], u0 | w, rho, sigma, -
+        pdat = rayq + kRQ;                   // pair table, 4 planes [4][64] float4: A[0:4] | A[4:8] | A[8], u0 | r2, rho, sigma, r3
         wave_stride = al4(pdat + 64 * 16);
         red = wave_base;                     // final reduction reuses the wave regions
         total = wave_base + kWaves * wave_stride;
@@ -1388,7 +1403,8 @@ __device__ __forceinline__ void load_pdat(const float* pd, int slot, float* A, f
     const float4 a = q4[0], c = q4[64], e = q4[128], g = q4[192];
     A[0] = a.x; A[1] = a.y; A[2] = a.z; A[3] = a.w; A[4] = c.x; A[5] = c.y; A[6] = c.z; A[7] = c.w; A[8] = e.x;
     u0[0] = e.y; u0[1] = e.z; u0[2] = e.w;
-    w = g.x; rho = g.y; sigma = g.z;
+    rho = g.y; sigma = g.z;
+    w = sigma * rho;   // (= P.w of the pair setup, bit for bit)
 }
 
 // grow[k] = dL/dhist[p,k] att[k] hscale[p], zero-padded to nr + kBPad.  Rows of nr % 4 == 0
@@ -1535,8 +1551,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_B
     const float f0log2 = log2f(1.0f + 1e-7f);
     const float rscale = k.opt.ray_scale;
 
-    float dA[9], dMu[3], dSig = 0.f;
-    for (int t = 0; t < 9; ++t) dA[t] = 0.f;
+    // shape accumulators (shape_acc: D = diag of dA A^T, K~ = its rotational part), dL/dmu, dL/dsigma
+    float sD[3] = {0.f, 0.f, 0.f}, sK[3] = {0.f, 0.f, 0.f}, dMu[3], dSig = 0.f;
     dMu[0] = dMu[1] = dMu[2] = 0.f;
     // this lane's Gaussian: record and feature row are re-read per wall point (L1/L2 hits) rather
     // than held in registers across the split (VGPR budget)
@@ -1605,7 +1621,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_B
             d4[0] = make_float4(P.A[0], P.A[1], P.A[2], P.A[3]);
             d4[64] = make_float4(P.A[4], P.A[5], P.A[6], P.A[7]);
             d4[128] = make_float4(P.A[8], P.u0[0], P.u0[1], P.u0[2]);
-            d4[192] = make_float4(P.w, P.rho, P.sigma, 0.f);
+            float r2, r3;
+            scale_ratios(P.A, r2, r3);
+            d4[192] = make_float4(r2, P.rho, P.sigma, r3);
         }
         // ray cache of the forward: cached pairs walk their recorded cells instead of enumerating
         unsigned long long cbits0 = 0ull, cbits1 = 0ull;
@@ -1970,12 +1988,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_B
                 for (int c = 0; c < 3; ++c) { gU[c] = gm * __shfl(rU[c], src); gV[c] = gm * __shfl(rV[c], src); }
                 const float gSig = gm * __shfl(rSig, src);
                 const float gRho = MODE == NLOSGR_MODE_NOOCL ? 0.f : gm * __shfl(rRho, src);
-                const int sij = __shfl(b.ij, src);
-                const int gij = got ? sij : 0;
-                const float2 th = tth[gij & 0xFFFF], ph = tph[gij >> 16];
-                const float d3[3] = {th.x * ph.x, th.x * ph.y, th.y};
-                for (int r = 0; r < 3; ++r)
-                    for (int c = 0; c < 3; ++c) dA[3 * r + c] += gV[r] * d3[c];
+                // the ray's v = A d (whitened direction) comes with its result: dL/dA += dL/dv d^T is
+                // accumulated as shape_acc(dL/dv, v) (the rotational part kept apart from the scales)
+                float gW[3];
+#pragma unroll
+                for (int c = 0; c < 3; ++c) gW[c] = __shfl(b.v[c], src);
+                const float4 rr = reinterpret_cast<const float4*>(pdat)[192 + lane];   // r2, rho, sigma, r3
+                shape_acc(gV, gW, rr.x, rr.w, sD, sK);
                 for (int r = 0; r < 3; ++r) dU0p[r] += gU[r];
                 if (MODE == NLOSGR_MODE_NOOCL) {
                     s0_pair += gSig;
@@ -1996,13 +2015,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_B
             drho_pair = s0_pair * wrs.z;
         }
         if (active && wpair > 0.f) {
-            const float4 ma = k.recs[gi].a;   // mu
-            const float q[3] = {px - ma.x, py - ma.y, pz - ma.z};
+            // dL/dA += dL/du0 (p - mu)^T, as shape_acc(dL/du0, u0) with u0 = A (p - mu) from the pair table
             const float4* d4 = reinterpret_cast<const float4*>(pdat) + lane;
-            const float4 a = d4[0], c = d4[64], e = d4[128];
+            const float4 a = d4[0], c = d4[64], e = d4[128], rr = d4[192];
             const float A[9] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w, e.x};
-            for (int r = 0; r < 3; ++r)
-                for (int cc = 0; cc < 3; ++cc) dA[3 * r + cc] += dU0p[r] * q[cc];
+            const float u0[3] = {e.y, e.z, e.w};
+            shape_acc(dU0p, u0, rr.x, rr.w, sD, sK);
             for (int cc = 0; cc < 3; ++cc) dMu[cc] -= A[cc] * dU0p[0] + A[3 + cc] * dU0p[1] + A[6 + cc] * dU0p[2];
         }
         if (active) k.drho[(size_t)(p - k.pb0) * k.g.ng + gio] = (wpair > 0.f && !(k.opt.flags & 64)) ? drho_pair : 0.f;
@@ -2017,7 +2035,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_B
             // workspace held, later batches add)
             float* dst = k.partial + ((size_t)split * k.g.ng + gi) * 32;
             float v[kBwdSlots];
-            for (int t = 0; t < 9; ++t) v[t] = dA[t];
+            for (int t = 0; t < 3; ++t) { v[t] = sD[t]; v[3 + t] = sK[t]; v[6 + t] = 0.f; }
             v[9] = dMu[0]; v[10] = dMu[1]; v[11] = dMu[2]; v[12] = dSig;
             if (k.accum)
                 for (int t = 0; t < kBwdSlots; ++t) v[t] += dst[t];
@@ -2030,7 +2048,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_B
     float* red = smem + L.red;
     {
         float* dst = red + (wave * 64 + lane) * kBwdSlots;
-        for (int t = 0; t < 9; ++t) dst[t] = dA[t];
+        for (int t = 0; t < 3; ++t) { dst[t] = sD[t]; dst[3 + t] = sK[t]; dst[6 + t] = 0.f; }
         dst[9] = dMu[0]; dst[10] = dMu[1]; dst[11] = dMu[2];
         dst[12] = dSig;
     }
@@ -2116,7 +2134,7 @@ __global__ __launch_bounds__(kBlock) void finish_kernel(KArgs k, float* d_mu, fl
         for (int t = 0; t < KM; ++t) acc[13 + t] += src[t];
         for (int t = 0; t < 3; ++t) acc[9 + t] += src[KM + t];
     }
-    chain_to_raw<PRESET>(k.g, i, acc, d_scaling, d_rot);
+    chain_to_raw_shape<PRESET>(k.g, i, acc, acc + 3, d_scaling, d_rot);
     d_mu[3 * i] = acc[9]; d_mu[3 * i + 1] = acc[10]; d_mu[3 * i + 2] = acc[11];
     const float sg = 1.0f / (1.0f + expf(-k.g.opacity[i]));
     d_opac[i] = acc[12] * sg * (1.0f - sg);
@@ -2244,6 +2262,13 @@ void launch_fwd(const KArgs& ka, size_t shm, hipStream_t s) {
     const bool tail = kCanTail && ka.opt.cutoff >= kTailCutoff && (!ka.counts || NLOSGR_FCOUNT_ON) &&
                       !(ka.opt.flags & NLOSGR_FLAG_MASKED_FWD) &&
                       (MODE != NLOSGR_MODE_NETF || ka.opt.c_deltaT <= kSmallX);
+    if constexpr (!RAYS && !CACHE) {
+        if (ka.counts) {   // nlosgr_count_support
+            if (tail) hipLaunchKernelGGL((count_kernel<PRESET, MODE, DENSE, kCanTail>), grid, dim3(kBlock), shm, s, ka);
+            else hipLaunchKernelGGL((count_kernel<PRESET, MODE, DENSE, false>), grid, dim3(kBlock), shm, s, ka);
+            return;
+        }
+    }
     if (tail) hipLaunchKernelGGL((fwd_kernel<PRESET, MODE, DENSE, RAYS, CACHE, kCanTail>), grid, dim3(kBlock), shm, s, ka);
     else hipLaunchKernelGGL((fwd_kernel<PRESET, MODE, DENSE, RAYS, CACHE>), grid, dim3(kBlock), shm, s, ka);
 }

@@ -7,7 +7,13 @@ Each positional argument is one variant (comma-separated NAME=VALUE pairs, '-' f
 JSON line: per variant fwd/bwd medians and the forward's rel-L2 against the first variant."""
 import argparse, dataclasses, hashlib, json, os, statistics, sys, time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path.insert(0, os.path.join(ROOT, 'nlos-gaussian-renderer_amd')); sys.path.insert(0, ROOT)
+# --pkg DIR: time another build of the package (e.g. ab/r5pkg, a previous round's Python + library)
+PKG = os.path.join(ROOT, 'nlos-gaussian-renderer_amd')
+if '--pkg' in sys.argv:
+    i = sys.argv.index('--pkg')
+    PKG = os.path.abspath(sys.argv[i + 1])
+    del sys.argv[i:i + 2]
+sys.path.insert(0, PKG); sys.path.insert(0, ROOT)
 import torch
 from nlosgr import GaussianParams, features_flat
 from nlosgr.volume import Scene, make_config

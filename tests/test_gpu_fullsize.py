@@ -242,7 +242,7 @@ def test_c3_trainstep_full_ng_accuracy():
         a, b = a.reshape(b.shape).double(), b.double()
         e = float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
         print(f"C3 TrainStep ordered backward vs unordered: {name} max err {e:.3e} of max")
-        assert e <= 2e-4, (name, e)
+        assert e <= 2e-5, (name, e)
 
 
 def test_c4_full_size_binint_vs_numerical():
