@@ -793,14 +793,16 @@ __device__ __forceinline__ void fwd_body(const KArgs& k) {
                 // rounds without one (all of them unless the bounds spread, see kFxBits) run the plain loop
                 const bool anyb = FX && wbright;
                 const int gb0 = d.pos & ~(VW - 1);
-                auto emit_l = [&](int kv, float v0, float v1) { emit2<FX>(reinterpret_cast<float2*>(hb) + kv, v0, v1); };
+                // (FX: every emitting lane is a winner, so its row starts at gb0 with no loser select)
+                float2* const hbw = reinterpret_cast<float2*>(FX ? hist + gb0 : hb);
+                auto emit_l = [&](int kv, float v0, float v1) { emit2<FX>(hbw + kv, v0, v1); };
                 auto emit_g = [&](int kv, float v0, float v1) {
                     if (brt) {
                         const int b = gb0 + VW * kv;
                         if (b < nr && v0 > 0.f) fx_gadd(grow + b, v0);
                         if (b + 1 < nr && v1 > 0.f) fx_gadd(grow + b + 1, v1);
                     } else {
-                        emit2<FX>(reinterpret_cast<float2*>(hb) + kv, v0, v1);
+                        emit2<FX>(hbw + kv, v0, v1);
                     }
                 };
                 if (TAIL && win && MODE == NLOSGR_MODE_NOOCL) {
@@ -1497,6 +1499,11 @@ __device__ __forceinline__ bool bray_setup(const float* pd, float2 th, float2 ph
     return true;
 }
 
+#ifndef NLOSGR_SHAPE_SENDER
+#define NLOSGR_SHAPE_SENDER 1
+#endif
+constexpr bool kShapeSender = NLOSGR_SHAPE_SENDER;   // see rD / rK in bwd_kernel
+
 // TAIL (culled no-occlusion histogram backward at cutoff >= kTailCutoff): the drain reads the upstream
 // row without the segment-end mask, see BV below
 
@@ -1653,7 +1660,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_B
         b.T = b.pre = b.dsig = b.drho = 0.f;
         b.S0b = b.S1b = b.S2b = b.dsigb = 0.f;
         // pending result of a finished ray: dL/du0, dL/dv, dsigma, drho
-        float rU[3] = {0.f, 0.f, 0.f}, rV[3] = {0.f, 0.f, 0.f}, rSig = 0.f, rRho = 0.f;
+        // kShapeSender: the ray's dL/dA contribution dL/dv d^T goes over as shape_acc's (D, K~), formed at the
+        // ray's end (rD, rK); otherwise dL/dv and v go over and the pair lane forms it per hand-off round
+        float rU[3] = {0.f, 0.f, 0.f}, rD[3] = {0.f, 0.f, 0.f}, rK[3] = {0.f, 0.f, 0.f}, rSig = 0.f, rRho = 0.f;
         while (true) {
             if (CACHE && qcount < 64 && __builtin_amdgcn_ballot_w64((cbits0 | cbits1) != 0ull)) {
                 wave_sync();
@@ -1953,10 +1962,20 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_B
                             // (the exp-free culled drain keeps D = drho / (sigma c dT) in b.drho)
                             rRho = !DENSE && (small_x || TAIL) ? b.drho * (cdt * b.sigma) : b.drho;
                         }
+                        float rV[3];
                         for (int r = 0; r < 3; ++r) {
                             const float zv = S0 * b.zs[r] + S1 * b.v[r];
                             rU[r] = -zv;
                             rV[r] = -(b.ts * zv + S1 * b.zs[r] + S2 * b.v[r]);
+                        }
+                        if (kShapeSender) {
+                            // dL/dA += dL/dv d^T, in whitened form shape_acc(dL/dv, v = A d) with the pair's
+                            // scale ratios (pair table plane 3), formed once here rather than per hand-off round
+                            const float4 rr = reinterpret_cast<const float4*>(pdat)[192 + b.slot];   // r2, rho, sigma, r3
+                            rD[0] = rD[1] = rD[2] = rK[0] = rK[1] = rK[2] = 0.f;
+                            shape_acc(rV, b.v, rr.x, rr.w, rD, rK);
+                        } else {
+                            rD[0] = rV[0]; rD[1] = rV[1]; rD[2] = rV[2];   // (dL/dv; v stays in b.v)
                         }
                         act = false;
                         pend = !(k.opt.flags & 32);   // flags 32 (diagnostics): drop results, no hand-off
@@ -1982,19 +2001,28 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_B
                 const int wpair = __builtin_amdgcn_ds_bpermute(b.slot << 2, wcl);
                 const bool won = pend && wpair == lane + 1;
                 const float gm = got ? 1.f : 0.f;
-                float gU[3], gV[3];
+                float gU[3];
                 // every lane must execute the bpermute: it cannot read lanes that are inactive in EXEC
+                if (kShapeSender) {
 #pragma unroll
-                for (int c = 0; c < 3; ++c) { gU[c] = gm * __shfl(rU[c], src); gV[c] = gm * __shfl(rV[c], src); }
+                    for (int c = 0; c < 3; ++c) {
+                        gU[c] = gm * __shfl(rU[c], src);
+                        sD[c] += gm * __shfl(rD[c], src);
+                        sK[c] += gm * __shfl(rK[c], src);
+                    }
+                } else {
+                    float gV[3], gW[3];
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) {
+                        gU[c] = gm * __shfl(rU[c], src);
+                        gV[c] = gm * __shfl(rD[c], src);
+                        gW[c] = __shfl(b.v[c], src);
+                    }
+                    const float4 rr = reinterpret_cast<const float4*>(pdat)[192 + lane];   // r2, rho, sigma, r3
+                    shape_acc(gV, gW, rr.x, rr.w, sD, sK);
+                }
                 const float gSig = gm * __shfl(rSig, src);
                 const float gRho = MODE == NLOSGR_MODE_NOOCL ? 0.f : gm * __shfl(rRho, src);
-                // the ray's v = A d (whitened direction) comes with its result: dL/dA += dL/dv d^T is
-                // accumulated as shape_acc(dL/dv, v) (the rotational part kept apart from the scales)
-                float gW[3];
-#pragma unroll
-                for (int c = 0; c < 3; ++c) gW[c] = __shfl(b.v[c], src);
-                const float4 rr = reinterpret_cast<const float4*>(pdat)[192 + lane];   // r2, rho, sigma, r3
-                shape_acc(gV, gW, rr.x, rr.w, sD, sK);
                 for (int r = 0; r < 3; ++r) dU0p[r] += gU[r];
                 if (MODE == NLOSGR_MODE_NOOCL) {
                     s0_pair += gSig;
