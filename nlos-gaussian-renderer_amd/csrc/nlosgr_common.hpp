@@ -219,8 +219,8 @@ __device__ __forceinline__ void scale_ratios(const float* A, float& r2, float& r
     const float n1 = A[0] * A[0] + A[1] * A[1] + A[2] * A[2];
     const float n2 = A[3] * A[3] + A[4] * A[4] + A[5] * A[5];
     const float n3 = A[6] * A[6] + A[7] * A[7] + A[8] * A[8];
-    r2 = n1 / n2;
-    r3 = n1 / n3;
+    r2 = n1 * __builtin_amdgcn_rcpf(n2);   // (the same instruction sequence in every kernel that calls it)
+    r3 = n1 * __builtin_amdgcn_rcpf(n3);
 }
 
 // The backward's shape accumulators (round 6).  A contribution to dL/dA is an outer product g b^T (g = dL/du0

@@ -841,39 +841,40 @@ __device__ __forceinline__ void fwd_body(const KArgs& k) {
                     }
                 }
                 nseg += NLOSGR_FCOUNT_ON ? 0u : (unsigned)__popcll(__builtin_amdgcn_ballot_w64(got));
-                if (FX) {
-                    const unsigned long long bm = __builtin_amdgcn_ballot_w64(take && act && brt);
-                    if (bm && lane == 0) atomicAdd(k.fx_info + 3, (int)__popcll(bm));
-                }
                 const int ntake = min(nidle, qcount);
                 qhead = (qhead + ntake) & (kRQ - 1);
                 qcount -= ntake;
-                // (netf keeps its start: its transmittance would have to be re-seeded)
-                if (FX && kFxShift > 0 && MODE != NLOSGR_MODE_NETF) fx_place(take && act && !brt, act && !brt, d);
-                if (FX && __builtin_amdgcn_ballot_w64(act && brt)) {
-                    // bright segments (kFxBits; none unless the amplitude bounds spread): drained here at once,
-                    // their values added as u64 integers straight into the wall point's global row, so the
-                    // LDS drain rounds below never branch on them
-                    bool bl = act && brt;
-                    while (__builtin_amdgcn_ballot_w64(bl)) {
-                        if (bl) {
-                            const int o = d.pos & (VW - 1), gb0 = d.pos & ~(VW - 1);
-                            float T = d.T;
-                            tail_round([&](int kv, float v0, float v1) {
-                                const int b = gb0 + VW * kv;
-                                if (b < nr && v0 > 0.f) fx_gadd(grow + b, v0);
-                                if (b + 1 < nr && v1 > 0.f) fx_gadd(grow + b + 1, v1);
-                            }, d.t, T);
-                            const int adv = kSteps - o;
-                            d.t += (float)adv;
-                            d.T = T;
-                            d.pos += adv;
-                            d.rem -= adv;
-                            bl = d.rem > 0;
+                if (FX) {
+                    const unsigned long long bm = __builtin_amdgcn_ballot_w64(act && brt);   // (only new lanes)
+                    if (bm) {
+                        // bright segments (kFxBits; none unless the amplitude bounds spread): drained here at
+                        // once, their values added as u64 integers straight into the wall point's global row,
+                        // so the LDS drain rounds below never branch on them
+                        if (lane == 0) atomicAdd(k.fx_info + 3, (int)__popcll(bm));
+                        bool bl = act && brt;
+                        while (__builtin_amdgcn_ballot_w64(bl)) {
+                            if (bl) {
+                                const int o = d.pos & (VW - 1), gb0 = d.pos & ~(VW - 1);
+                                float T = d.T;
+                                tail_round([&](int kv, float v0, float v1) {
+                                    const int b = gb0 + VW * kv;
+                                    if (b < nr && v0 > 0.f) fx_gadd(grow + b, v0);
+                                    if (b + 1 < nr && v1 > 0.f) fx_gadd(grow + b + 1, v1);
+                                }, d.t, T);
+                                const int adv = kSteps - o;
+                                d.t += (float)adv;
+                                d.T = T;
+                                d.pos += adv;
+                                d.rem -= adv;
+                                bl = d.rem > 0;
+                            }
                         }
+                        act = act && !brt;
+                        brt = false;
                     }
-                    act = act && !brt;
                 }
+                // (netf keeps its start: its transmittance would have to be re-seeded)
+                if (FX && kFxShift > 0 && MODE != NLOSGR_MODE_NETF) fx_place(take && act, act, d);
             }
             const bool anyact = __builtin_amdgcn_ballot_w64(act) != 0;
             if (!anyact) {
