@@ -589,6 +589,149 @@ __device__ __forceinline__ void fx_place(bool newl, bool act, Drain& d) {
     }
 }
 
+// One TAIL drain round of a lane's segment (the QUADF histograms at cutoff >= kTailCutoff): kSteps values from
+// the even bin at or below pos (slot 0 before pos adds 0 in a segment's first round), every pair of bins to
+// emit(kv, v0, v1); t = d.t, T = the round's copy of d.T (netf: updated).  The drain rounds emit into the LDS
+// histogram; FX bright segments (kFxBits) run it in fx_bright_drain, emitting into the global u64 row.
+constexpr int kVW = 2;   // bins per LDS access of the vector drain (float2 / packed u64)
+template <int MODE, class Emit>
+__device__ __forceinline__ void tail_round(const Drain& d, const float t, float& T, Emit&& emit) {
+    const int o = d.pos & (kVW - 1);
+    if (MODE == NLOSGR_MODE_NOOCL) {
+        // the recurrence is seeded at pos (inside the support: a seed one bin further out can
+        // underflow for Gaussians much narrower than a bin); slot 0 before pos (o = 1) adds 0
+        float cur = fast_exp2(fmaf(d.ga, t * t, d.al));
+        float q = fast_exp2(d.ga * fmaf(2.f, t, 1.f));
+        const float cc = fast_exp2(2.f * d.ga);
+        {
+#pragma unroll
+            for (int kv = 0; kv < kSteps / kVW; ++kv) {
+                const float v0 = (kv == 0 && o) ? 0.f : cur;
+                if (kv == 0) {
+                    cur = o ? cur : cur * q;
+                    q = o ? q : q * cc;
+                } else {
+                    cur *= q;
+                    q *= cc;
+                }
+                const float v1 = cur;
+                cur *= q;
+                q *= cc;
+                emit(kv, v0, v1);
+            }
+        }
+    } else if (MODE == NLOSGR_MODE_BININT) {
+        // bin-integrated (C4), TAIL: the average of exp(-beta^2 t^2) over the bin [t - 1/2, t + 1/2]
+        // (t in bins from the closest approach, beta = dr sqrt(a / 2)) is g(t) (1 + sum_n g^(2n)(t) /
+        // (2^2n (2n+1)!) / g(t)) = g(t) P(beta^2 t^2), P a cubic from the n <= 3 terms: relative error
+        // <= 7e-8 for beta <= kBetaSeries (a Gaussian wider than 1.4 bins along the ray), so g comes
+        // from the exp2 recurrence as in the numerical drain and each bin costs a cubic instead of
+        // two erfc.  Narrower rays (beta > kBetaSeries) take the erf difference, when a round holds one.
+        const float b = d.beta * d.beta;
+        const float c3 = b * b * b * (1.0f / 5040.0f);
+        const float c2 = b * b * fmaf(b, -1.0f / 672.0f, 1.0f / 120.0f);
+        const float c1 = b * fmaf(b, fmaf(b, 1.0f / 448.0f, -1.0f / 40.0f), 1.0f / 6.0f);
+        const float c0 = fmaf(b, fmaf(b, fmaf(b, -1.0f / 2688.0f, 1.0f / 160.0f), -1.0f / 12.0f), 1.0f);
+        const float t0 = t - (float)o;    // t of slot 0
+        float cur = fast_exp2(fmaf(d.ga, t * t, d.al));
+        float q = fast_exp2(d.ga * fmaf(2.f, t, 1.f));
+        const float cc = fast_exp2(2.f * d.ga);
+        const bool series = d.beta <= kBetaSeries;
+        const bool anyerf = __builtin_amdgcn_ballot_w64(!series) != 0;   // (EXEC = the winners)
+        const float pref = fast_exp2(d.al) * (0.88622692545275801f * frcp(d.beta));
+        {
+#pragma unroll
+            for (int kv = 0; kv < kSteps / kVW; ++kv) {
+                float v[kVW];
+#pragma unroll
+                for (int jj = 0; jj < kVW; ++jj) {
+                    const int jslot = kVW * kv + jj;
+                    const float tj = t0 + (float)jslot;
+                    const float u = b * tj * tj;
+                    float val = cur * fmaf(u, fmaf(u, fmaf(u, c3, c2), c1), c0);
+                    if (anyerf && !series) {
+                        const float x0 = d.beta * (tj - 0.5f), x1 = d.beta * (tj + 0.5f);
+                        const float e0 = erfcf(fabsf(x0)), e1 = erfcf(fabsf(x1));
+                        const float df = x0 >= 0.f ? e0 - e1 : (x1 <= 0.f ? e1 - e0 : 2.0f - e0 - e1);
+                        val = pref * df;
+                    }
+                    const bool pre = kv == 0 && jj < o;   // slot before pos (first round of a segment)
+                    v[jj] = pre ? 0.f : val;
+                    cur = pre ? cur : cur * q;
+                    q = pre ? q : q * cc;
+                }
+                emit(kv, v[0], v[1]);
+            }
+        }
+    } else {
+        // netf, TAIL: out_k = w c dT sin(theta) pdf_k T_k, T_{k+1} = T_k (exp(-sigma pdf_k c dT)
+        // + 1e-7), two bins per float2 read-add-write; slot 0 before pos (o = 1, a segment's
+        // first round) adds 0 and leaves T as it is
+        float cur = fast_exp2(fmaf(d.ga, t * t, d.al));   // seeded at pos (see above)
+        // the recurrence runs on p~_m = pdf_m c0^m and the transmittance on T~_m = T_m / c0^m (m = bins
+        // past pos, c0 = kTf0 = 1 + 1e-7): v_m = T~_m p~_m = T_m pdf_m and T~_{m+1} = T~_m f_m / c0 =
+        // T~_m + v_m g(p~_m) with g the cubic's p-terms over c0, one fma per bin (T rescaled per round)
+        float q = fast_exp2(d.ga * fmaf(2.f, t, 1.f)) * kTf0;
+        const float cc = fast_exp2(2.f * d.ga);
+        // the TAIL netf forward runs only at c dT <= kSmallX, so x = sigma pdf c dT <= 1/64 and
+        // exp(-x) + 1e-7 is the cubic the backward uses (truncation x^4 / 24 <= 2.5e-9): no exp.
+        // As a cubic in pdf: f = c0 + e1 pdf + e2 pdf^2 + e3 pdf^3, e1 = -sx, e2 = sx^2 / 2, e3 =
+        // -sx^3 / 6 (the 1e-7 folded into c0: 1 + 1e-7 rounds to 1 + 2^-23, 1.9e-8 per bin); g takes
+        // p~ for pdf, 1 + 2.4e-6 relative at most within a round: f off by <= 2.4e-6 x per bin
+        const float sx = d.sc;
+        const float e1 = -sx * kRTf0, e2 = 0.5f * sx * sx * kRTf0, e3 = (-1.0f / 6.0f) * sx * sx * sx * kRTf0;
+        auto gfac = [e1, e2, e3](float pv) { return fmaf(pv, fmaf(pv, e3, e2), e1); };
+        {
+#pragma unroll
+            for (int kv = 0; kv < kSteps / kVW; ++kv) {
+                const float p0 = cur;
+                if (kv == 0) {
+                    cur = o ? cur : cur * q;
+                    q = o ? q : q * cc;
+                } else {
+                    cur *= q;
+                    q *= cc;
+                }
+                const float p1 = cur;
+                cur *= q;
+                q *= cc;
+                // T carries w c dT sin(theta) (set at the segment's start); slot 0 before pos adds 0
+                // and (v0 = 0) leaves T as it is
+                const float v0 = (kv == 0 && o) ? 0.f : T * p0;
+                T = fmaf(v0, gfac(p0), T);
+                const float v1 = T * p1;
+                T = fmaf(v1, gfac(p1), T);
+                emit(kv, v0, v1);
+            }
+        }
+        T *= o ? kTfPow<kSteps - 1>() : kTfPow<kSteps>();   // T = T~ c0^(bins advanced)
+    }
+}
+
+#ifndef NLOSGR_FX_BRIGHT
+#define NLOSGR_FX_BRIGHT 1
+#endif
+// FX bright segment (kFxBits), called by the lanes that took one at refill: the whole segment, round by round,
+// as u64 integer adds straight into the wall point's global row.  Out of line, so the drain loop's registers
+// and schedule do not carry this rare path.
+template <int MODE>
+__device__ __attribute__((noinline)) void fx_bright_drain(Drain& d, unsigned long long* grow, int nr) {
+    while (d.rem > 0) {
+        const int o = d.pos & (kVW - 1), gb0 = d.pos & ~(kVW - 1);
+        float T = d.T;
+        tail_round<MODE>(d, d.t, T, [&](int kv, float v0, float v1) {
+            const int b = gb0 + kVW * kv;
+            if (b < nr && v0 > 0.f) fx_gadd(grow + b, v0);
+            if (b + 1 < nr && v1 > 0.f) fx_gadd(grow + b + 1, v1);
+        });
+        const int adv = kSteps - o;
+        d.t += (float)adv;
+        d.T = T;
+        d.pos += adv;
+        d.rem -= adv;
+    }
+}
+
 template <int PRESET, int MODE, bool DENSE, bool RAYS, bool CACHE, bool TAIL, bool FX>
 __device__ __forceinline__ void fwd_body(const KArgs& k) {
     extern __shared__ __align__(16) float smem[];
@@ -652,123 +795,7 @@ __device__ __forceinline__ void fwd_body(const KArgs& k) {
     bool act = false;
     int qhead = 0, qcount = 0;
 
-    // One TAIL drain round of this lane's segment (the QUADF histograms at cutoff >= kTailCutoff): kSteps values
-    // from the even bin at or below pos (slot 0 before pos adds 0 in a segment's first round), every pair of bins
-    // to emit(kv, v0, v1); t = d.t, T = the round's copy of d.T (netf: updated).  The drain rounds emit into the
-    // LDS histogram; FX bright segments (kFxBits) run it at refill, emitting into the global u64 row.
-    constexpr int VW = 2;   // bins per LDS access of the vector drain (float2 / packed u64)
-    auto tail_round = [&](auto emit, const float t, float& T) {
-        const int o = d.pos & (VW - 1);
-        if (MODE == NLOSGR_MODE_NOOCL) {
-            // the recurrence is seeded at pos (inside the support: a seed one bin further out can
-            // underflow for Gaussians much narrower than a bin); slot 0 before pos (o = 1) adds 0
-            float cur = fast_exp2(fmaf(d.ga, t * t, d.al));
-            float q = fast_exp2(d.ga * fmaf(2.f, t, 1.f));
-            const float cc = fast_exp2(2.f * d.ga);
-            {
-#pragma unroll
-                for (int kv = 0; kv < kSteps / VW; ++kv) {
-                    const float v0 = (kv == 0 && o) ? 0.f : cur;
-                    if (kv == 0) {
-                        cur = o ? cur : cur * q;
-                        q = o ? q : q * cc;
-                    } else {
-                        cur *= q;
-                        q *= cc;
-                    }
-                    const float v1 = cur;
-                    cur *= q;
-                    q *= cc;
-                    emit(kv, v0, v1);
-                }
-            }
-        } else if (MODE == NLOSGR_MODE_BININT) {
-            // bin-integrated (C4), TAIL: the average of exp(-beta^2 t^2) over the bin [t - 1/2, t + 1/2]
-            // (t in bins from the closest approach, beta = dr sqrt(a / 2)) is g(t) (1 + sum_n g^(2n)(t) /
-            // (2^2n (2n+1)!) / g(t)) = g(t) P(beta^2 t^2), P a cubic from the n <= 3 terms: relative error
-            // <= 7e-8 for beta <= kBetaSeries (a Gaussian wider than 1.4 bins along the ray), so g comes
-            // from the exp2 recurrence as in the numerical drain and each bin costs a cubic instead of
-            // two erfc.  Narrower rays (beta > kBetaSeries) take the erf difference, when a round holds one.
-            const float b = d.beta * d.beta;
-            const float c3 = b * b * b * (1.0f / 5040.0f);
-            const float c2 = b * b * fmaf(b, -1.0f / 672.0f, 1.0f / 120.0f);
-            const float c1 = b * fmaf(b, fmaf(b, 1.0f / 448.0f, -1.0f / 40.0f), 1.0f / 6.0f);
-            const float c0 = fmaf(b, fmaf(b, fmaf(b, -1.0f / 2688.0f, 1.0f / 160.0f), -1.0f / 12.0f), 1.0f);
-            const float t0 = t - (float)o;    // t of slot 0
-            float cur = fast_exp2(fmaf(d.ga, t * t, d.al));
-            float q = fast_exp2(d.ga * fmaf(2.f, t, 1.f));
-            const float cc = fast_exp2(2.f * d.ga);
-            const bool series = d.beta <= kBetaSeries;
-            const bool anyerf = __builtin_amdgcn_ballot_w64(!series) != 0;   // (EXEC = the winners)
-            const float pref = fast_exp2(d.al) * (0.88622692545275801f * frcp(d.beta));
-            {
-#pragma unroll
-                for (int kv = 0; kv < kSteps / VW; ++kv) {
-                    float v[VW];
-#pragma unroll
-                    for (int jj = 0; jj < VW; ++jj) {
-                        const int jslot = VW * kv + jj;
-                        const float tj = t0 + (float)jslot;
-                        const float u = b * tj * tj;
-                        float val = cur * fmaf(u, fmaf(u, fmaf(u, c3, c2), c1), c0);
-                        if (anyerf && !series) {
-                            const float x0 = d.beta * (tj - 0.5f), x1 = d.beta * (tj + 0.5f);
-                            const float e0 = erfcf(fabsf(x0)), e1 = erfcf(fabsf(x1));
-                            const float df = x0 >= 0.f ? e0 - e1 : (x1 <= 0.f ? e1 - e0 : 2.0f - e0 - e1);
-                            val = pref * df;
-                        }
-                        const bool pre = kv == 0 && jj < o;   // slot before pos (first round of a segment)
-                        v[jj] = pre ? 0.f : val;
-                        cur = pre ? cur : cur * q;
-                        q = pre ? q : q * cc;
-                    }
-                    emit(kv, v[0], v[1]);
-                }
-            }
-        } else {
-            // netf, TAIL: out_k = w c dT sin(theta) pdf_k T_k, T_{k+1} = T_k (exp(-sigma pdf_k c dT)
-            // + 1e-7), two bins per float2 read-add-write; slot 0 before pos (o = 1, a segment's
-            // first round) adds 0 and leaves T as it is
-            float cur = fast_exp2(fmaf(d.ga, t * t, d.al));   // seeded at pos (see above)
-            // the recurrence runs on p~_m = pdf_m c0^m and the transmittance on T~_m = T_m / c0^m (m = bins
-            // past pos, c0 = kTf0 = 1 + 1e-7): v_m = T~_m p~_m = T_m pdf_m and T~_{m+1} = T~_m f_m / c0 =
-            // T~_m + v_m g(p~_m) with g the cubic's p-terms over c0, one fma per bin (T rescaled per round)
-            float q = fast_exp2(d.ga * fmaf(2.f, t, 1.f)) * kTf0;
-            const float cc = fast_exp2(2.f * d.ga);
-            // the TAIL netf forward runs only at c dT <= kSmallX, so x = sigma pdf c dT <= 1/64 and
-            // exp(-x) + 1e-7 is the cubic the backward uses (truncation x^4 / 24 <= 2.5e-9): no exp.
-            // As a cubic in pdf: f = c0 + e1 pdf + e2 pdf^2 + e3 pdf^3, e1 = -sx, e2 = sx^2 / 2, e3 =
-            // -sx^3 / 6 (the 1e-7 folded into c0: 1 + 1e-7 rounds to 1 + 2^-23, 1.9e-8 per bin); g takes
-            // p~ for pdf, 1 + 2.4e-6 relative at most within a round: f off by <= 2.4e-6 x per bin
-            const float sx = d.sc;
-            const float e1 = -sx * kRTf0, e2 = 0.5f * sx * sx * kRTf0, e3 = (-1.0f / 6.0f) * sx * sx * sx * kRTf0;
-            auto gfac = [e1, e2, e3](float pv) { return fmaf(pv, fmaf(pv, e3, e2), e1); };
-            {
-#pragma unroll
-                for (int kv = 0; kv < kSteps / VW; ++kv) {
-                    const float p0 = cur;
-                    if (kv == 0) {
-                        cur = o ? cur : cur * q;
-                        q = o ? q : q * cc;
-                    } else {
-                        cur *= q;
-                        q *= cc;
-                    }
-                    const float p1 = cur;
-                    cur *= q;
-                    q *= cc;
-                    // T carries w c dT sin(theta) (set at the segment's start); slot 0 before pos adds 0
-                    // and (v0 = 0) leaves T as it is
-                    const float v0 = (kv == 0 && o) ? 0.f : T * p0;
-                    T = fmaf(v0, gfac(p0), T);
-                    const float v1 = T * p1;
-                    T = fmaf(v1, gfac(p1), T);
-                    emit(kv, v0, v1);
-                }
-            }
-            T *= o ? kTfPow<kSteps - 1>() : kTfPow<kSteps>();   // T = T~ c0^(bins advanced)
-        }
-    };
+    constexpr int VW = kVW;
 
     for (int base = g_lo + wave * 64;; base += kBlock) {
         const bool have = base < g_hi;         // wave-uniform
@@ -851,24 +878,7 @@ __device__ __forceinline__ void fwd_body(const KArgs& k) {
                         // once, their values added as u64 integers straight into the wall point's global row,
                         // so the LDS drain rounds below never branch on them
                         if (lane == 0) atomicAdd(k.fx_info + 3, (int)__popcll(bm));
-                        bool bl = act && brt;
-                        while (__builtin_amdgcn_ballot_w64(bl)) {
-                            if (bl) {
-                                const int o = d.pos & (VW - 1), gb0 = d.pos & ~(VW - 1);
-                                float T = d.T;
-                                tail_round([&](int kv, float v0, float v1) {
-                                    const int b = gb0 + VW * kv;
-                                    if (b < nr && v0 > 0.f) fx_gadd(grow + b, v0);
-                                    if (b + 1 < nr && v1 > 0.f) fx_gadd(grow + b + 1, v1);
-                                }, d.t, T);
-                                const int adv = kSteps - o;
-                                d.t += (float)adv;
-                                d.T = T;
-                                d.pos += adv;
-                                d.rem -= adv;
-                                bl = d.rem > 0;
-                            }
-                        }
+                        if (NLOSGR_FX_BRIGHT && act && brt) fx_bright_drain<MODE>(d, grow, nr);
                         act = act && !brt;
                         brt = false;
                     }
@@ -935,7 +945,7 @@ __device__ __forceinline__ void fwd_body(const KArgs& k) {
                 if (TAIL && win) {
                     // (FX: every emitting lane is a winner, so its row starts at the even bin with no loser select)
                     float2* const hbw = reinterpret_cast<float2*>(FX ? hist + (d.pos & ~(VW - 1)) : hb);
-                    tail_round([&](int kv, float v0, float v1) { emit2<FX>(hbw + kv, v0, v1); }, t, T);
+                    tail_round<MODE>(d, t, T, [&](int kv, float v0, float v1) { emit2<FX>(hbw + kv, v0, v1); });
                 } else if (win) {
                     float cur = fast_exp2(fmaf(d.ga, t * t, d.al));
                     float q = fast_exp2(d.ga * fmaf(2.f, t, 1.f));

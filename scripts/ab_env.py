@@ -25,6 +25,8 @@ ap.add_argument('--cutoff', type=float, default=5.7)
 ap.add_argument('--reps', type=int, default=3)
 ap.add_argument('--bwd', action='store_true')
 ap.add_argument('--mode', default='noocl')
+ap.add_argument('--flags', type=int, default=0, help='nlosgr_options.flags (A/B variants, phase ablation)')
+ap.add_argument('--order', default='given', choices=('given', 'slab'), help="Gaussian order (TrainStep's slab orders)")
 ap.add_argument('variants', nargs='+')
 a = ap.parse_args()
 ng, H, T = {'C3': (100_000, 128, 1024), 'S1': (20_000, 32, 512), 'C2': (50_000, 64, 512)}[a.config]
@@ -33,7 +35,11 @@ scene = Scene(H=H, W=H, T=T, ns=32)
 m = GaussianParams.synthetic(ng, 3, preset='cuda', device=dev, seed=0)
 geo = scene.geometry(dev, 'cuda', a.mode)
 args = (m._mu.detach(), m._scaling.detach(), m._rotation.detach(), m._opacity.detach(), features_flat(m).detach(), geo)
-cfg = dataclasses.replace(make_config(m, scene, 'cuda', cutoff=a.cutoff), mode=a.mode)
+cfg = dataclasses.replace(make_config(m, scene, 'cuda', cutoff=a.cutoff), mode=a.mode, flags=a.flags)
+if a.order == 'slab':   # the forward's order in TrainStep (8 depth slabs, largest log-scale within a slab)
+    from nlosgr.train import slab_order, wall_centroid
+    perm = slab_order(args[0], None, 8, 1, size=args[1].max(1).values, centroid=wall_centroid(geo.wall))
+    args = tuple(t[perm].contiguous() for t in args[:5]) + (args[5],)
 
 
 def setenv(v):
