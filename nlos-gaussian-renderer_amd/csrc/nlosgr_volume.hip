@@ -78,7 +78,9 @@ struct KArgs {
     int accum;                   // backward batches after the first add into the partial slabs
     unsigned long long* hfx;     // forward FX drain: fixed-point histogram [P][nr] (u64, integer adds)
     int* fx_info;                // forward FX drain: [0] unit exponent E (fx_unit_kernel), [1] E of the launch's
-                                 // largest bound, [2] LDS flushes, [3] bright segments (see kFxBits)
+                                 // largest bound, [2] LDS flushes, [3] bright segments, [4] bright Gaussians
+    const float* fx_bound;       // forward FX drain: amplitude bound per Gaussian [ng] (fx_bound_kernel)
+    const int* fx_blist;         // forward FX drain: the bright Gaussians (fx_blist_kernel), [fx_info[4]]
 };
 
 // ray cache: a pair whose (theta, phi) candidate box has at most 128 cells records which cells
@@ -490,7 +492,8 @@ constexpr float kBetaSeries = 0.5f;   // bin-integrated TAIL drain: series bin a
 // fx_reduce_kernel scales it to floats.
 constexpr int kFxBits = 24;
 constexpr int kFxRange = 20;                 // E <= E(max bound) + kFxRange: u64 terms < 2^(kFxBits + kFxRange)
-constexpr float kFxBright = 16777216.0f;     // 2^kFxBits: segments with a larger peak take the global path
+constexpr float kFxBright = 16777216.0f;     // 2^kFxBits
+constexpr float kFxMargin = 1.002f;          // segment peak <= bound x 2^E x kFxMargin (binint 1.001, netf (1+1e-7)^nr)
 constexpr float kFxLimit = 4294967040.0f;   // largest float below 2^32
 constexpr int kFxBins = 256;                 // bound histogram: one bin per binary exponent (float bits >> 23)
 constexpr int kFxTailBytes = 2048;           // workspace tail of the FX area: bins u32 [256] | info int [8]
@@ -592,7 +595,7 @@ __device__ __forceinline__ void fx_place(bool newl, bool act, Drain& d) {
 // One TAIL drain round of a lane's segment (the QUADF histograms at cutoff >= kTailCutoff): kSteps values from
 // the even bin at or below pos (slot 0 before pos adds 0 in a segment's first round), every pair of bins to
 // emit(kv, v0, v1); t = d.t, T = the round's copy of d.T (netf: updated).  The drain rounds emit into the LDS
-// histogram; FX bright segments (kFxBits) run it in fx_bright_drain, emitting into the global u64 row.
+// histogram, or (the bright launch, BR) the wall point's global u64 row.
 constexpr int kVW = 2;   // bins per LDS access of the vector drain (float2 / packed u64)
 template <int MODE, class Emit>
 __device__ __forceinline__ void tail_round(const Drain& d, const float t, float& T, Emit&& emit) {
@@ -708,31 +711,7 @@ __device__ __forceinline__ void tail_round(const Drain& d, const float t, float&
     }
 }
 
-#ifndef NLOSGR_FX_BRIGHT
-#define NLOSGR_FX_BRIGHT 1
-#endif
-// FX bright segment (kFxBits), called by the lanes that took one at refill: the whole segment, round by round,
-// as u64 integer adds straight into the wall point's global row.  Out of line, so the drain loop's registers
-// and schedule do not carry this rare path.
-template <int MODE>
-__device__ __attribute__((noinline)) void fx_bright_drain(Drain& d, unsigned long long* grow, int nr) {
-    while (d.rem > 0) {
-        const int o = d.pos & (kVW - 1), gb0 = d.pos & ~(kVW - 1);
-        float T = d.T;
-        tail_round<MODE>(d, d.t, T, [&](int kv, float v0, float v1) {
-            const int b = gb0 + kVW * kv;
-            if (b < nr && v0 > 0.f) fx_gadd(grow + b, v0);
-            if (b + 1 < nr && v1 > 0.f) fx_gadd(grow + b + 1, v1);
-        });
-        const int adv = kSteps - o;
-        d.t += (float)adv;
-        d.T = T;
-        d.pos += adv;
-        d.rem -= adv;
-    }
-}
-
-template <int PRESET, int MODE, bool DENSE, bool RAYS, bool CACHE, bool TAIL, bool FX>
+template <int PRESET, int MODE, bool DENSE, bool RAYS, bool CACHE, bool TAIL, bool FX, bool BR = false>
 __device__ __forceinline__ void fwd_body(const KArgs& k) {
     extern __shared__ __align__(16) float smem[];
     const int nr = k.geo.nr, nt = k.geo.nt, np_ = k.geo.np;
@@ -749,8 +728,10 @@ __device__ __forceinline__ void fwd_body(const KArgs& k) {
     // Gaussian split of this wall point (grid.y; 64-aligned ranges): partial histograms are summed
     // in split order by hist_reduce_kernel when gridDim.y > 1
     const int gsplit = blockIdx.y, nsp = gridDim.y;
-    const int gper = (((k.g.ng + nsp - 1) / nsp) + 63) & ~63;
-    const int g_lo = gsplit * gper, g_hi = min(k.g.ng, g_lo + gper);
+    // BR (the bright launch): the Gaussians of the bright list instead of all of them
+    const int gcount = BR ? k.fx_info[4] : k.g.ng;
+    const int gper = (((gcount + nsp - 1) / nsp) + 63) & ~63;
+    const int g_lo = gsplit * gper, g_hi = min(gcount, g_lo + gper);
 
     for (int t = threadIdx.x; t < nt; t += blockDim.x)
         tth[t] = make_float2(k.geo.sin_theta[(size_t)p * nt + t], k.geo.cos_theta[(size_t)p * nt + t]);
@@ -775,7 +756,6 @@ __device__ __forceinline__ void fwd_body(const KArgs& k) {
     const float fxS = FX ? fast_exp2(fxE) : 1.f;   // exact: fxE is an integer
     float fthr = kFxLimit / 64.f;   // wave-uniform
     float fpk = 0.f, fxs = 0.f;     // this lane's segment peak, and its peaks since the last check
-    bool brt = false;               // FX: this lane's segment is bright (global u64 adds, see kFxBits)
     unsigned long long* const grow = FX ? k.hfx + (size_t)p * nr : nullptr;
     unsigned* hist32 = reinterpret_cast<unsigned*>(hist);
     const int nfx = nr + kSteps + 2;   // fields a round can reach (bins past nr are pad)
@@ -810,13 +790,16 @@ __device__ __forceinline__ void fwd_body(const KArgs& k) {
             const int gi = base + lane;
             // the record is loaded ahead of the setup math; the SH coefficients are read from global
             // inside the albedo sum (a register copy of the row spilled the setup at 80 VGPRs)
-            const int gl = min(gi, k.g.ng - 1);
+            const int gl = BR ? k.fx_blist[min(gi, g_hi - 1)] : min(gi, k.g.ng - 1);
             const GaussRec nrec = k.recs[gl];
+            // FX: Gaussians whose bound reaches 2^kFxBits units (bright, see kFxBits) are the bright launch's
+            // (the same comparison in fx_blist_kernel)
+            const bool bright = FX && !BR && !(k.fx_bound[gl] * fxS * kFxMargin < kFxBright);
             if (gi < g_hi) {
                 float mu[3];
                 load_rec(nrec, P, mu);
                 pair_setup<PRESET, DENSE>(k, k.g.features + (size_t)gl * k.g.k_feat, mu, px, py, pz, lin, mc2, P);
-                more = (P.w > 0.f) && P.i0 <= P.i1 && P.j0 <= P.j1;
+                more = (P.w > 0.f) && P.i0 <= P.i1 && P.j0 <= P.j1 && !bright;
                 lw = more ? flog2(P.w) + fxE : 0.f;
                 sc = P.sigma * cdt;
                 wc = more ? P.w * cdt * fxS : 0.f;   // netf: the value's scale rides on T
@@ -862,8 +845,6 @@ __device__ __forceinline__ void fwd_body(const KArgs& k) {
                         // the segment's largest value (t = 0), in units (netf: T <= its start x (1 + 1e-7)^nr)
                         fpk = MODE == NLOSGR_MODE_NETF ? d.T * fast_exp2(d.al) * 1.001f
                                                        : fast_exp2(d.al) * (MODE == NLOSGR_MODE_BININT ? 1.001f : 1.f);
-                        brt = !(fpk < kFxBright);   // (non-finite peaks too)
-                        if (brt) fpk = 0.f;         // bright: no LDS adds
                         fxs += fpk;
                     }
                 }
@@ -871,20 +852,8 @@ __device__ __forceinline__ void fwd_body(const KArgs& k) {
                 const int ntake = min(nidle, qcount);
                 qhead = (qhead + ntake) & (kRQ - 1);
                 qcount -= ntake;
-                if (FX) {
-                    const unsigned long long bm = __builtin_amdgcn_ballot_w64(act && brt);   // (only new lanes)
-                    if (bm) {
-                        // bright segments (kFxBits; none unless the amplitude bounds spread): drained here at
-                        // once, their values added as u64 integers straight into the wall point's global row,
-                        // so the LDS drain rounds below never branch on them
-                        if (lane == 0) atomicAdd(k.fx_info + 3, (int)__popcll(bm));
-                        if (NLOSGR_FX_BRIGHT && act && brt) fx_bright_drain<MODE>(d, grow, nr);
-                        act = act && !brt;
-                        brt = false;
-                    }
-                }
                 // (netf keeps its start: its transmittance would have to be re-seeded)
-                if (FX && kFxShift > 0 && MODE != NLOSGR_MODE_NETF) fx_place(take && act, act, d);
+                if (FX && !BR && kFxShift > 0 && MODE != NLOSGR_MODE_NETF) fx_place(take && act, act, d);
             }
             const bool anyact = __builtin_amdgcn_ballot_w64(act) != 0;
             if (!anyact) {
@@ -895,7 +864,7 @@ __device__ __forceinline__ void fwd_body(const KArgs& k) {
             // claim distinct start keys (distinct addresses; vector drain: distinct start pairs)
             constexpr bool QUAD = QUADF;
             bool win = act;   // FX: integer adds, no claims
-            if (FX && __builtin_amdgcn_ballot_w64(fxs > fthr)) {
+            if (FX && !BR && __builtin_amdgcn_ballot_w64(fxs > fthr)) {
                 // a lane passed its share of the headroom: read the fields' true maximum (and move
                 // them to the global u64 histogram once it passes 2^31)
                 wave_sync();
@@ -945,7 +914,16 @@ __device__ __forceinline__ void fwd_body(const KArgs& k) {
                 if (TAIL && win) {
                     // (FX: every emitting lane is a winner, so its row starts at the even bin with no loser select)
                     float2* const hbw = reinterpret_cast<float2*>(FX ? hist + (d.pos & ~(VW - 1)) : hb);
-                    tail_round<MODE>(d, t, T, [&](int kv, float v0, float v1) { emit2<FX>(hbw + kv, v0, v1); });
+                    if (BR) {   // bright launch: u64 integer adds straight into the wall point's global row
+                        const int gb0 = d.pos & ~(VW - 1);
+                        tail_round<MODE>(d, t, T, [&](int kv, float v0, float v1) {
+                            const int b = gb0 + VW * kv;
+                            if (b < nr && v0 > 0.f) fx_gadd(grow + b, v0);
+                            if (b + 1 < nr && v1 > 0.f) fx_gadd(grow + b + 1, v1);
+                        });
+                    } else {
+                        tail_round<MODE>(d, t, T, [&](int kv, float v0, float v1) { emit2<FX>(hbw + kv, v0, v1); });
+                    }
                 } else if (win) {
                     float cur = fast_exp2(fmaf(d.ga, t * t, d.al));
                     float q = fast_exp2(d.ga * fmaf(2.f, t, 1.f));
@@ -1070,6 +1048,10 @@ __device__ __forceinline__ void fwd_body(const KArgs& k) {
             atomicAdd(k.counts + 2, ns);
         }
     }
+    if (BR) {   // bright segments taken (nlosgr_fx_info)
+        if (lane == 0 && nseg) atomicAdd(k.fx_info + 3, (int)nseg);
+        return;
+    }
     __syncthreads();
     if (FX) {
         // the 4 waves' fields of each bin -> one integer add into the wall point's global u64 row
@@ -1095,6 +1077,12 @@ __device__ __forceinline__ void fwd_body(const KArgs& k) {
 template <int PRESET, int MODE, bool DENSE, bool RAYS, bool CACHE, bool TAIL = false, bool FX = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) void fwd_kernel(KArgs k) {
     fwd_body<PRESET, MODE, DENSE, RAYS, CACHE, TAIL, FX>(k);
+}
+// FX bright launch (BR): the Gaussians whose amplitude bound reaches 2^kFxBits units (fx_blist_kernel), every
+// segment added as u64 integers straight into the wall point's global row (kFxBits); usually an empty list
+template <int PRESET, int MODE>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) void fx_bright_kernel(KArgs k) {
+    fwd_body<PRESET, MODE, false, false, false, true, true, true>(k);
 }
 // nlosgr_count_support's launch of the same body under its own name, so profiles tell it apart from the
 // timed forward by identity
@@ -1123,7 +1111,8 @@ __global__ __launch_bounds__(kBlock) void hist_reduce_kernel(const float* __rest
 // bounds are not counted: a NaN Gaussian is skipped by the drains (w > 0 fails) and must not move the unit
 // of the others; an infinite one takes the bright path (saturating, kFxBits).
 template <int PRESET>
-__global__ __launch_bounds__(kBlock) void fx_bound_kernel(nlosgr_gaussians g, float ascale, unsigned* bins) {
+__global__ __launch_bounds__(kBlock) void fx_bound_kernel(nlosgr_gaussians g, float ascale, unsigned* bins,
+                                                         float* bound) {
     __shared__ unsigned lh[kFxBins];
     lh[threadIdx.x] = 0u;
     __syncthreads();
@@ -1140,6 +1129,8 @@ __global__ __launch_bounds__(kBlock) void fx_bound_kernel(nlosgr_gaussians g, fl
         }
         const float a = sig * (0.5f + 1.05f * sh) * 1.001f * ascale;   // ascale: the mode's factor (netf: c dT)
         if (a > 0.f && a < 3.0e38f) atomicAdd(&lh[__float_as_uint(a) >> 23], 1u);
+        // per Gaussian: 0 for NaN (skipped everywhere), +inf past the float range (the bright launch saturates)
+        bound[i] = a >= 3.0e38f ? INFINITY : (a > 0.f ? a : 0.f);
     }
     __syncthreads();
     const unsigned c = lh[threadIdx.x];
@@ -1180,6 +1171,15 @@ __global__ __launch_bounds__(kFxBins) void fx_unit_kernel(const unsigned* __rest
         info[0] = e;
         info[1] = emax;
     }
+}
+
+// FX: the bright Gaussians (bound x 2^E x kFxMargin >= 2^kFxBits, the comparison of fwd_body) appended to a
+// list (any order: the bright launch's sums are integers); info[4] = their number
+__global__ __launch_bounds__(kBlock) void fx_blist_kernel(const float* __restrict__ bound, int ng, int* info, int* blist) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= ng) return;
+    const float fxS = ldexpf(1.0f, info[0]);
+    if (!(bound[i] * fxS * kFxMargin < kFxBright)) blist[atomicAdd(info + 4, 1)] = i;
 }
 
 // FX: hist[p,t] = (u64 count x 2^-E) x att[t] x hscale[p]
@@ -2307,6 +2307,8 @@ void launch_fwd(const KArgs& ka, size_t shm, hipStream_t s) {
                   !RAYS && !CACHE) {
         if (ka.hfx) {   // run_fwd decided the fixed-point TAIL drain (fx_eligible)
             hipLaunchKernelGGL((fwd_kernel<PRESET, MODE, DENSE, RAYS, CACHE, true, true>), grid, dim3(kBlock), shm, s, ka);
+            // the bright Gaussians' launch (one split per wall point; its list is usually empty)
+            hipLaunchKernelGGL((fx_bright_kernel<PRESET, MODE>), dim3(ka.geo.nwall, 1), dim3(kBlock), shm, s, ka);
             return;
         }
     }
@@ -2392,13 +2394,16 @@ int fwd_nsplit(const nlosgr_gaussians* g, const nlosgr_geometry* geo) {
     if (ns > 8) ns = 8;
     return ns < 1 ? 1 : ns;
 }
-// forward partials: float [nfsplit][P][nr] (float drains) or, for the FX drain, u64 [P][nr] + the
-// bound histogram and info words (kFxTailBytes) at the end
-size_t fpart_bytes(const nlosgr_gaussians* g, const nlosgr_geometry* geo) {
+// forward partials: float [nfsplit][P][nr] (float drains) or, for the FX drain, u64 [P][nr]; then the FX
+// tail (bound histogram and info words, kFxTailBytes), the per-Gaussian bounds and the bright list
+size_t fx_tail_off(const nlosgr_gaussians* g, const nlosgr_geometry* geo) {
     const int ns = fwd_nsplit(g, geo);
     const size_t fl = ns > 1 ? (size_t)ns * geo->nwall * geo->nr * sizeof(float) : 0;
     const size_t fx = (size_t)geo->nwall * geo->nr * sizeof(unsigned long long);
-    return align_up(fl > fx ? fl : fx) + kFxTailBytes;
+    return align_up(fl > fx ? fl : fx);
+}
+size_t fpart_bytes(const nlosgr_gaussians* g, const nlosgr_geometry* geo) {
+    return fx_tail_off(g, geo) + kFxTailBytes + 2 * align_up((size_t)g->ng * sizeof(float));
 }
 // the fixed-point TAIL drain serves the culled no-occlusion histogram at cutoff >= kTailCutoff
 // (NLOSGR_FLAG_FLOAT_DRAIN: the float claim drain instead, A/B)
@@ -2447,20 +2452,26 @@ int run_fwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_
     const bool fx = g->ng > 0 && fx_eligible(opt, dense, rays, counts != nullptr, hist_out != nullptr, ka.cmask != nullptr);
     if (fx) {
         ka.hfx = (unsigned long long*)fpart;
-        unsigned* bins = (unsigned*)(fpart + fpart_bytes(g, geo) - kFxTailBytes);
+        unsigned* bins = (unsigned*)(fpart + fx_tail_off(g, geo));
         ka.fx_info = (int*)(bins + kFxBins);
+        float* bound = (float*)((char*)bins + kFxTailBytes);
+        int* blist = (int*)((char*)bound + align_up((size_t)g->ng * sizeof(float)));
+        ka.fx_bound = bound;
+        ka.fx_blist = blist;
         ka.nfsplit = nfs;
         HIPCHK(hipMemsetAsync(ka.hfx, 0, (size_t)geo->nwall * geo->nr * sizeof(unsigned long long), s));
         HIPCHK(hipMemsetAsync(bins, 0, kFxBins * sizeof(unsigned) + 8 * sizeof(int), s));
         const int nb = (g->ng + kBlock - 1) / kBlock;
         const float ascale = opt->mode == NLOSGR_MODE_NETF ? opt->c_deltaT : 1.0f;
         if (g->preset == NLOSGR_PRESET_TORCH)
-            hipLaunchKernelGGL(fx_bound_kernel<NLOSGR_PRESET_TORCH>, dim3(nb), dim3(kBlock), 0, s, *g, ascale, bins);
+            hipLaunchKernelGGL(fx_bound_kernel<NLOSGR_PRESET_TORCH>, dim3(nb), dim3(kBlock), 0, s, *g, ascale, bins, bound);
         else
-            hipLaunchKernelGGL(fx_bound_kernel<NLOSGR_PRESET_CUDA>, dim3(nb), dim3(kBlock), 0, s, *g, ascale, bins);
+            hipLaunchKernelGGL(fx_bound_kernel<NLOSGR_PRESET_CUDA>, dim3(nb), dim3(kBlock), 0, s, *g, ascale, bins, bound);
         HIPCHK(hipGetLastError());
         hipLaunchKernelGGL(fx_unit_kernel, dim3(1), dim3(kFxBins), 0, s, bins, ka.fx_info,
                            (opt->flags & NLOSGR_FLAG_FX_MAXUNIT) ? 1 : 0);
+        HIPCHK(hipGetLastError());
+        hipLaunchKernelGGL(fx_blist_kernel, dim3(nb), dim3(kBlock), 0, s, bound, g->ng, ka.fx_info, blist);
         HIPCHK(hipGetLastError());
     } else if (hist_out && nfs > 1 && g->ng > 0) {
         ka.hpart = (float*)fpart;
@@ -2579,7 +2590,7 @@ int nlosgr_fx_info(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const 
     if (!workspace || !info_out) return set_err(NLOSGR_E_INVALID, "null workspace or info_out");
     if (tiles_engine(opt) || g->ng == 0) return set_err(NLOSGR_E_UNSUPPORTED, "fx_info: pair-major forward with ng > 0");
     const char* fpart = fpart_ptr(g, geo, opt, const_cast<void*>(workspace));
-    const char* info = fpart + fpart_bytes(g, geo) - kFxTailBytes + kFxBins * sizeof(unsigned);
+    const char* info = fpart + fx_tail_off(g, geo) + kFxBins * sizeof(unsigned);
     HIPCHK(hipMemcpyAsync(info_out, info, 4 * sizeof(int32_t), hipMemcpyDeviceToDevice, (hipStream_t)hip_stream));
     return NLOSGR_OK;
 }
