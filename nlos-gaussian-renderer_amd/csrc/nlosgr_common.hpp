@@ -79,8 +79,12 @@ inline BatchBudgets& batch_budgets() {
 // ------------------------------------------------------------------------------------------
 // preprocess: raw params -> A = diag(1/s~) R', sigma, s_max, N = A^T A
 // ------------------------------------------------------------------------------------------
+// fxb / fxinfo (the forward's fixed-point drain, nlosgr_volume.hip kFxBits): a Gaussian whose amplitude bound
+// reaches 2^24 units (fxb[i] x 2^E x 1.002 >= 2^24, E = fxinfo[0]) is stored with a negative sigma, so the
+// main fixed-point launch skips it (w = sigma rho <= 0) and the bright launch takes |sigma|
 template <int PRESET>
-__global__ __launch_bounds__(kBlock) void preprocess_kernel(nlosgr_gaussians g, GaussRec* recs) {
+__global__ __launch_bounds__(kBlock) void preprocess_kernel(nlosgr_gaussians g, GaussRec* recs, const float* fxb,
+                                                           const int* fxinfo) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= g.ng) return;
     float S[3] = {g.scaling[3 * i], g.scaling[3 * i + 1], g.scaling[3 * i + 2]};
@@ -98,7 +102,9 @@ __global__ __launch_bounds__(kBlock) void preprocess_kernel(nlosgr_gaussians g, 
     }
     const float smax = fmaxf(a.st[0], fmaxf(a.st[1], a.st[2]));
     GaussRec rec;
-    rec.a = make_float4(g.mu[3 * i], g.mu[3 * i + 1], g.mu[3 * i + 2], a.sigma);
+    float sg = a.sigma;
+    if (fxb && !(fxb[i] * ldexpf(1.0f, fxinfo[0]) * 1.002f < 16777216.0f)) sg = -sg;
+    rec.a = make_float4(g.mu[3 * i], g.mu[3 * i + 1], g.mu[3 * i + 2], sg);
     rec.b = make_float4(A[0], A[1], A[2], A[3]);
     rec.c = make_float4(A[4], A[5], A[6], A[7]);
     rec.d = make_float4(A[8], smax, N[0], N[1]);
@@ -106,12 +112,13 @@ __global__ __launch_bounds__(kBlock) void preprocess_kernel(nlosgr_gaussians g, 
     recs[i] = rec;
 }
 
-inline void launch_preprocess(const nlosgr_gaussians* g, GaussRec* recs, hipStream_t s) {
+inline void launch_preprocess(const nlosgr_gaussians* g, GaussRec* recs, hipStream_t s, const float* fxb = nullptr,
+                              const int* fxinfo = nullptr) {
     const int nb = (g->ng + kBlock - 1) / kBlock;
     if (g->preset == NLOSGR_PRESET_TORCH)
-        hipLaunchKernelGGL(preprocess_kernel<NLOSGR_PRESET_TORCH>, dim3(nb), dim3(kBlock), 0, s, *g, recs);
+        hipLaunchKernelGGL(preprocess_kernel<NLOSGR_PRESET_TORCH>, dim3(nb), dim3(kBlock), 0, s, *g, recs, fxb, fxinfo);
     else
-        hipLaunchKernelGGL(preprocess_kernel<NLOSGR_PRESET_CUDA>, dim3(nb), dim3(kBlock), 0, s, *g, recs);
+        hipLaunchKernelGGL(preprocess_kernel<NLOSGR_PRESET_CUDA>, dim3(nb), dim3(kBlock), 0, s, *g, recs, fxb, fxinfo);
 }
 
 // sig-sigma axis-aligned box of Gaussian i: bbox_compute.cuh:23-71 (cuda: s = exp(S) mod, identity for a

@@ -792,14 +792,15 @@ __device__ __forceinline__ void fwd_body(const KArgs& k) {
             // inside the albedo sum (a register copy of the row spilled the setup at 80 VGPRs)
             const int gl = BR ? k.fx_blist[min(gi, g_hi - 1)] : min(gi, k.g.ng - 1);
             const GaussRec nrec = k.recs[gl];
-            // FX: Gaussians whose bound reaches 2^kFxBits units (bright, see kFxBits) are the bright launch's
-            // (the same comparison in fx_blist_kernel)
-            const bool bright = FX && !BR && !(k.fx_bound[gl] * fxS * kFxMargin < kFxBright);
+            // FX: Gaussians whose bound reaches 2^kFxBits units (bright, see kFxBits) are the bright launch's:
+            // preprocess_kernel stored them with a negative sigma (the same comparison as fx_blist_kernel), so
+            // here w <= 0 skips them; the bright launch takes |sigma|
             if (gi < g_hi) {
                 float mu[3];
                 load_rec(nrec, P, mu);
+                if (BR) P.sigma = fabsf(P.sigma);
                 pair_setup<PRESET, DENSE>(k, k.g.features + (size_t)gl * k.g.k_feat, mu, px, py, pz, lin, mc2, P);
-                more = (P.w > 0.f) && P.i0 <= P.i1 && P.j0 <= P.j1 && !bright;
+                more = (P.w > 0.f) && P.i0 <= P.i1 && P.j0 <= P.j1;
                 lw = more ? flog2(P.w) + fxE : 0.f;
                 sc = P.sigma * cdt;
                 wc = more ? P.w * cdt * fxS : 0.f;   // netf: the value's scale rides on T
@@ -2180,9 +2181,16 @@ __global__ __launch_bounds__(kBlock) void finish_kernel(KArgs k, float* d_mu, fl
     if (i >= k.g_hi) return;
     float acc[13 + KM];
     for (int t = 0; t < 13 + KM; ++t) acc[t] = 0.f;
-    for (int s = 0; s < k.nsplit; ++s) {
-        const float* src = k.partial + ((size_t)s * k.g.ng + i) * 32;
-        for (int t = 0; t < kBwdSlots; ++t) acc[t] += src[t];
+    {
+        // the wall-point splits' partials summed in fp64 (fixed order): the rotational shape sums are small
+        // differences of the splits' contributions
+        double sum[kBwdSlots];
+        for (int t = 0; t < kBwdSlots; ++t) sum[t] = 0.0;
+        for (int s = 0; s < k.nsplit; ++s) {
+            const float* src = k.partial + ((size_t)s * k.g.ng + i) * 32;
+            for (int t = 0; t < kBwdSlots; ++t) sum[t] += (double)src[t];
+        }
+        for (int t = 0; t < kBwdSlots; ++t) acc[t] = (float)sum[t];
     }
     for (int s = 0; s < k.nsh; ++s) {   // view-direction chain (sh_kernel)
         const float* src = k.shpart + ((size_t)s * k.g.ng + i) * kShPart;
@@ -2478,7 +2486,8 @@ int run_fwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_
         ka.nfsplit = nfs;
     }
     if (g->ng > 0) {
-        launch_preprocess(g, (GaussRec*)workspace, s);
+        // (FX: the bright Gaussians get a negative sigma in the records, see preprocess_kernel)
+        launch_preprocess(g, (GaussRec*)workspace, s, ka.hfx ? ka.fx_bound : nullptr, ka.fx_info);
         HIPCHK(hipGetLastError());
     }
     const size_t shm = (size_t)FwdLayout(geo->nr, geo->nt, geo->np, fx).total * sizeof(float);
