@@ -592,6 +592,46 @@ __device__ __forceinline__ void fx_place(bool newl, bool act, Drain& d) {
     }
 }
 
+// FX refill permutation (no-occlusion FX drain).  Every active lane advances the same kSteps / 2 words per
+// round, so the bank pair (word mod 16) of each segment relative to the others is fixed for its life: the
+// conflicts of a ds_add_u64 (serviced in 4 groups of 16 lanes, bank pair = word mod 16; scripts/lds_fx_probe.hip
+// modes 11-16) are set by which segments share a 16-lane group.  At refill the segments are re-dealt over the
+// lanes: sorted by (residue, lane) with the idle lanes last, and position s goes to lane 16 (s mod 4) + s / 4,
+// so the segments of one residue land in different groups (a residue held by c segments costs ceil(c / 4) per
+// group, the least any assignment can reach) and the active lanes spread evenly over the groups.  The sort is
+// bit-serial over ballots (5 key bits, no per-residue tables); the state moves with ds_permute (a bijection).
+// The per-lane headroom sums (fxs) stay: their total still bounds every field.
+#ifndef NLOSGR_FX_DIAG_NOCONFLICT
+#define NLOSGR_FX_DIAG_NOCONFLICT 0
+#endif
+#ifndef NLOSGR_FXPERM
+#define NLOSGR_FXPERM 0
+#endif
+constexpr bool kFxPerm = NLOSGR_FXPERM;
+__device__ __forceinline__ void fx_perm(bool& newl, bool& act, Drain& d, float& fpk) {
+    const unsigned key = act ? (unsigned)((d.pos >> 1) & 15) : 16u;
+    unsigned long long eq = ~0ull, lt = 0ull;
+#pragma unroll
+    for (int b = 4; b >= 0; --b) {
+        const bool mine = (key >> b) & 1u;
+        const unsigned long long B = __builtin_amdgcn_ballot_w64(mine);
+        lt |= mine ? (eq & ~B) : 0ull;
+        eq &= mine ? B : ~B;
+    }
+    const int s = __popcll(lt) + lanes_below(eq);
+    const int a4 = (((s & 3) << 4) | (s >> 2)) << 2;
+    const int ri = act ? (d.rem | (newl ? (1 << 30) : 0)) : 0;
+    const int ri2 = __builtin_amdgcn_ds_permute(a4, ri);
+    d.pos = __builtin_amdgcn_ds_permute(a4, d.pos);
+    d.t = __int_as_float(__builtin_amdgcn_ds_permute(a4, __float_as_int(d.t)));
+    d.ga = __int_as_float(__builtin_amdgcn_ds_permute(a4, __float_as_int(d.ga)));
+    d.al = __int_as_float(__builtin_amdgcn_ds_permute(a4, __float_as_int(d.al)));
+    fpk = __int_as_float(__builtin_amdgcn_ds_permute(a4, __float_as_int(fpk)));
+    act = ri2 != 0;
+    newl = (ri2 >> 30) & 1;
+    d.rem = ri2 & ((1 << 30) - 1);
+}
+
 // One TAIL drain round of a lane's segment (the QUADF histograms at cutoff >= kTailCutoff): kSteps values from
 // the even bin at or below pos (slot 0 before pos adds 0 in a segment's first round), every pair of bins to
 // emit(kv, v0, v1); t = d.t, T = the round's copy of d.T (netf: updated).  The drain rounds emit into the LDS
@@ -854,7 +894,9 @@ __device__ __forceinline__ void fwd_body(const KArgs& k) {
                 qhead = (qhead + ntake) & (kRQ - 1);
                 qcount -= ntake;
                 // (netf keeps its start: its transmittance would have to be re-seeded)
-                if (FX && !BR && kFxShift > 0 && MODE != NLOSGR_MODE_NETF) fx_place(take && act, act, d);
+                bool newl = take && act;
+                if (FX && !BR && kFxPerm && MODE == NLOSGR_MODE_NOOCL) fx_perm(newl, act, d, fpk);
+                if (FX && !BR && kFxShift > 0 && MODE != NLOSGR_MODE_NETF) fx_place(newl, act, d);
             }
             const bool anyact = __builtin_amdgcn_ballot_w64(act) != 0;
             if (!anyact) {
@@ -914,7 +956,11 @@ __device__ __forceinline__ void fwd_body(const KArgs& k) {
                 const int lim = remw + o;   // slot j is in the segment iff o <= j < lim
                 if (TAIL && win) {
                     // (FX: every emitting lane is a winner, so its row starts at the even bin with no loser select)
+#if NLOSGR_FX_DIAG_NOCONFLICT   // diagnostics (wrong sums): every lane on its own word residue, no bank conflicts
+                    float2* const hbw = reinterpret_cast<float2*>(FX ? hist + 2 * lane : hb);
+#else
                     float2* const hbw = reinterpret_cast<float2*>(FX ? hist + (d.pos & ~(VW - 1)) : hb);
+#endif
                     if (BR) {   // bright launch: u64 integer adds straight into the wall point's global row
                         const int gb0 = d.pos & ~(VW - 1);
                         tail_round<MODE>(d, t, T, [&](int kv, float v0, float v1) {

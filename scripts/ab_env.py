@@ -26,7 +26,9 @@ ap.add_argument('--reps', type=int, default=3)
 ap.add_argument('--bwd', action='store_true')
 ap.add_argument('--mode', default='noocl')
 ap.add_argument('--flags', type=int, default=0, help='nlosgr_options.flags (A/B variants, phase ablation)')
-ap.add_argument('--order', default='given', choices=('given', 'slab'), help="Gaussian order (TrainStep's slab orders)")
+ap.add_argument('--order', default='given', choices=('given', 'slab', 'train'),
+                help="Gaussian order: slab = TrainStep's forward order for both passes; train = TrainStep's "
+                     "forward order (8 depth slabs) for the forward and its backward order (8 x 4 x 4 cells)")
 ap.add_argument('variants', nargs='+')
 a = ap.parse_args()
 ng, H, T = {'C3': (100_000, 128, 1024), 'S1': (20_000, 32, 512), 'C2': (50_000, 64, 512)}[a.config]
@@ -36,9 +38,13 @@ m = GaussianParams.synthetic(ng, 3, preset='cuda', device=dev, seed=0)
 geo = scene.geometry(dev, 'cuda', a.mode)
 args = (m._mu.detach(), m._scaling.detach(), m._rotation.detach(), m._opacity.detach(), features_flat(m).detach(), geo)
 cfg = dataclasses.replace(make_config(m, scene, 'cuda', cutoff=a.cutoff), mode=a.mode, flags=a.flags)
-if a.order == 'slab':   # the forward's order in TrainStep (8 depth slabs, largest log-scale within a slab)
+args_b = args
+if a.order in ('slab', 'train'):   # the forward's order in TrainStep (8 depth slabs, largest log-scale within a slab)
     from nlosgr.train import slab_order, wall_centroid
-    perm = slab_order(args[0], None, 8, 1, size=args[1].max(1).values, centroid=wall_centroid(geo.wall))
+    cen = wall_centroid(geo.wall)
+    perm = slab_order(args[0], None, 8, 1, size=args[1].max(1).values, centroid=cen)
+    pb = slab_order(args[0], None, 8, 4, size=args[1].max(1).values, centroid=cen) if a.order == 'train' else perm
+    args_b = tuple(t[pb].contiguous() for t in args[:5]) + (args[5],)
     args = tuple(t[perm].contiguous() for t in args[:5]) + (args[5],)
 
 
@@ -73,7 +79,7 @@ for rep in range(a.reps + 1):
         tb = 0.0
         if a.bwd:
             t0 = time.perf_counter()
-            d = render_backward(*args, cfg, grad_hist=grad)
+            d = render_backward(*args_b, cfg, grad_hist=grad)
             torch.cuda.synchronize()
             tb = (time.perf_counter() - t0) * 1e3
             if rep == 0:   # bitwise fingerprint of the gradients (compare across processes / libraries)

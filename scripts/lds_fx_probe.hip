@@ -17,6 +17,10 @@
 //            16-lane group, lanes l and l + 16 on the same word mod 32 (which lane grouping banks it?)
 //   mode 12: ds_add_u64, lane l at word base + (l mod 32) + 64 (l / 32): distinct mod 32 within each half
 //   mode 13: ds_add_u64, lane l at word base + 16 (l mod 4) + (l / 4): 16-lane groups hold 4 runs of 4
+//   mode 14: ds_add_u64, lane l at word base + 2 (l mod 16) + 64 (l / 16): 2-way mod 16, distinct mod 32 per group
+//   mode 15: ds_add_u64, lane l at word base + (l mod 16) + 16 (l / 16) + 48 (l / 32): groups of 16 distinct
+//            mod 16; lanes l and l + 16 distinct mod 32; lanes l and l + 32 equal mod 64 words
+//   mode 16: ds_add_u64, lane l at word base + 16 l: all 64 lanes on one word residue mod 16 (16-way per group)
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdint.h>
@@ -34,22 +38,25 @@ __global__ __launch_bounds__(256) void bench(float* out, int seed) {
     constexpr bool ATOM = MODE == 1 || MODE == 3 || MODE == 4 || (MODE >= 6 && MODE != 10);
     constexpr bool PATTERN = MODE >= 11;
     constexpr int SPREAD = (MODE == 2 || MODE == 3) ? 48 : ((MODE == 4 || MODE == 5) ? 12 : 0);
-    __shared__ __align__(16) unsigned h32[4 * (kBins + 192)];
-    for (int t = threadIdx.x; t < 4 * (kBins + 192); t += 256) h32[t] = 0u;
+    __shared__ __align__(16) unsigned h32[4 * (kBins + 640)];
+    for (int t = threadIdx.x; t < 4 * (kBins + 640); t += 256) h32[t] = 0u;
     (void)PATTERN;
     __syncthreads();
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     unsigned st = (unsigned)(lane * 2654435761u) ^ (unsigned)(seed + blockIdx.x * 7919);
     float v = 1.0f + lane * 1e-3f;
-    const int wbase = wave * (kBins + 192);
+    const int wbase = wave * (kBins + 640);
     for (int it = 0; it < kIters; ++it) {
         st = st * 1664525u + 1013904223u;
         int pos;
         if (PATTERN) {
             const int b = (int)(__builtin_amdgcn_readfirstlane((st >> 8) % (kBins - 300)) & ~1);
             const int w = MODE == 11 ? (lane % 16) + 32 * (lane / 16)
-                        : MODE == 12 ? (lane % 32) + 64 * (lane / 32) : 16 * (lane % 4) + lane / 4;
-            pos = b + 2 * (w % 128);
+                        : MODE == 12 ? (lane % 32) + 64 * (lane / 32)
+                        : MODE == 13 ? 16 * (lane % 4) + lane / 4
+                        : MODE == 14 ? 2 * (lane % 16) + 64 * (lane / 16)
+                        : MODE == 15 ? (lane % 16) + 16 * (lane / 16) + 48 * (lane / 32) : 16 * lane;
+            pos = b + 2 * (w % 256);
         } else if (MODE == 6 || MODE == 9) {
             pos = (int)(__builtin_amdgcn_readfirstlane((st >> 8) % (kBins - 160)) & ~1) + 2 * lane;
         } else if (SPREAD) {
@@ -87,7 +94,7 @@ __global__ __launch_bounds__(256) void bench(float* out, int seed) {
     }
     __syncthreads();
     float s = 0.f;
-    for (int t = threadIdx.x; t < 4 * (kBins + 192); t += 256) s += (float)(h32[t] & 0xffff);
+    for (int t = threadIdx.x; t < 4 * (kBins + 640); t += 256) s += (float)(h32[t] & 0xffff);
     out[blockIdx.x * 256 + threadIdx.x] = s;
 }
 
@@ -109,7 +116,7 @@ void run(float* d) {
 int main() {
     float* d;
     hipMalloc(&d, kBlocks * 256 * sizeof(float));
-    run<0>(d); run<1>(d); run<2>(d); run<3>(d); run<4>(d); run<5>(d); run<6>(d); run<7>(d); run<8>(d); run<9>(d); run<10>(d); run<11>(d); run<12>(d); run<13>(d);
+    run<0>(d); run<1>(d); run<2>(d); run<3>(d); run<4>(d); run<5>(d); run<6>(d); run<7>(d); run<8>(d); run<9>(d); run<10>(d); run<11>(d); run<12>(d); run<13>(d); run<14>(d); run<15>(d); run<16>(d);
     hipFree(d);
     return 0;
 }

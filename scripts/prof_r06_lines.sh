@@ -4,9 +4,12 @@
 # with and without the tile bins.   LINES="occl_aabb aabb occl netf diag" bash scripts/prof_r06_lines.sh
 set -o pipefail
 O=gpurun_out/lines_r06; mkdir -p $O
-run() {   # name, timeout, bench args...
+export TMPDIR=/tmp
+run() {   # name, timeout, bench args...  (under rocprofv3 --kernel-trace --stats: kernel stats beside the line)
   local n=$1 t=$2; shift 2
-  NLOSGR_BENCH_PROGRESS=1 timeout -k 10 $t python bench.py "$@" > $O/$n.json 2> $O/$n.err || { tail -3 $O/$n.err; return 1; }
+  rm -rf /tmp/kt_$n
+  NLOSGR_BENCH_PROGRESS=1 timeout -k 10 $t rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/kt_$n -o prof -- python3 bench.py "$@" > $O/$n.json 2> $O/$n.err || { tail -3 $O/$n.err; return 1; }
+  cp $(find /tmp/kt_$n -name "*kernel_stats.csv" | head -1) $O/${n}_kernel_stats.csv
   tail -1 $O/$n.json | cut -c1-240
 }
 for l in ${LINES:-occl_aabb aabb occl netf diag}; do
