@@ -490,6 +490,9 @@ constexpr float kBetaSeries = 0.5f;   // bin-integrated TAIL drain: series bin a
 // the u64 row in global memory (integer atomics) and zeroes them.  At the end each workgroup adds its 4
 // waves' fields to the global u64 histogram [P][nr] (all Gaussian splits of a wall point meet there), and
 // fx_reduce_kernel scales it to floats.
+#ifdef NLOSGR_FXCOUNT
+__device__ unsigned long long g_fdbg[8];
+#endif
 constexpr int kFxBits = 24;
 constexpr int kFxRange = 20;                 // E <= E(max bound) + kFxRange: u64 terms < 2^(kFxBits + kFxRange)
 constexpr float kFxBright = 16777216.0f;     // 2^kFxBits
@@ -607,19 +610,74 @@ __device__ __forceinline__ void fx_place(bool newl, bool act, Drain& d) {
 #ifndef NLOSGR_FXPERM
 #define NLOSGR_FXPERM 0
 #endif
-constexpr bool kFxPerm = NLOSGR_FXPERM;
+constexpr bool kFxPerm = NLOSGR_FXPERM != 0;
+constexpr int kFxPermMode = NLOSGR_FXPERM;   // 1: deal, 2: levels
 __device__ __forceinline__ void fx_perm(bool& newl, bool& act, Drain& d, float& fpk) {
-    const unsigned key = act ? (unsigned)((d.pos >> 1) & 15) : 16u;
-    unsigned long long eq = ~0ull, lt = 0ull;
+    const unsigned res = (unsigned)((d.pos >> 1) & 15);
+    const unsigned long long am = __builtin_amdgcn_ballot_w64(act);
+    int dst;
+    if (kFxPermMode == 1) {
+        // deal: sorted by (residue, lane), idle lanes last; position s -> lane 16 (s mod 4) + s / 4
+        const unsigned key = act ? res : 16u;
+        unsigned long long eq = ~0ull, lt = 0ull;
 #pragma unroll
-    for (int b = 4; b >= 0; --b) {
-        const bool mine = (key >> b) & 1u;
-        const unsigned long long B = __builtin_amdgcn_ballot_w64(mine);
-        lt |= mine ? (eq & ~B) : 0ull;
-        eq &= mine ? B : ~B;
+        for (int b = 4; b >= 0; --b) {
+            const bool mine = (key >> b) & 1u;
+            const unsigned long long B = __builtin_amdgcn_ballot_w64(mine);
+            lt |= mine ? (eq & ~B) : 0ull;
+            eq &= mine ? B : ~B;
+        }
+        const int s = __popcll(lt) + lanes_below(eq);
+        dst = ((s & 3) << 4) | (s >> 2);
+    } else if (kFxPermMode == 3) {
+        // rank mod 4: the segment of rank j among its residue's goes to group j mod 4 (a residue held by c
+        // segments costs ceil((c - g) / 4) in group g: the sum over groups is the largest c, the least any
+        // assignment reaches); a group past 16 lanes spills its last lanes, then the idle lanes, into the
+        // other groups' free slots (group 3 first)
+        unsigned long long eq = am;
+#pragma unroll
+        for (int b = 3; b >= 0; --b) {
+            const bool mine = (res >> b) & 1u;
+            const unsigned long long B = __builtin_amdgcn_ballot_w64(mine);
+            eq &= mine ? B : ~B;
+        }
+        const int g = act ? (lanes_below(eq) & 3) : 4;
+        const unsigned long long G0 = __builtin_amdgcn_ballot_w64(g == 0), G1 = __builtin_amdgcn_ballot_w64(g == 1),
+                                 G2 = __builtin_amdgcn_ballot_w64(g == 2), G3 = __builtin_amdgcn_ballot_w64(g == 3);
+        const int N0 = min(__popcll(G0), 16), N1 = min(__popcll(G1), 16), N2 = min(__popcll(G2), 16),
+                  N3 = min(__popcll(G3), 16);
+        const unsigned long long Gk = g == 0 ? G0 : (g == 1 ? G1 : (g == 2 ? G2 : G3));
+        const int ig = lanes_below(Gk);
+        const bool spill = g == 4 || ig >= 16;
+        const unsigned long long SP = __builtin_amdgcn_ballot_w64(spill && g < 4);
+        const int f = g < 4 ? lanes_below(SP) : __popcll(SP) + lanes_below(~am);
+        const int F3 = 16 - N3, F32 = F3 + 16 - N2, F321 = F32 + 16 - N1;
+        const int fd = f < F3 ? 48 + N3 + f : (f < F32 ? 32 + N2 + (f - F3) : (f < F321 ? 16 + N1 + (f - F32) : N0 + (f - F321)));
+        dst = spill ? fd : 16 * g + ig;
+    } else {
+        // levels: the segment of rank k among its residue's (k < 4) goes to group k, at the index of its
+        // residue among that level's (one segment per residue: conflict-free); ranks >= 4 and then the
+        // idle lanes fill the groups' remaining slots, group 3 first
+        unsigned long long eq = am, lt = 0ull;
+#pragma unroll
+        for (int b = 3; b >= 0; --b) {
+            const bool mine = (res >> b) & 1u;
+            const unsigned long long B = __builtin_amdgcn_ballot_w64(mine);
+            lt |= mine ? (eq & ~B) : 0ull;
+            eq &= mine ? B : ~B;
+        }
+        const int lvl = act ? min(lanes_below(eq), 4) : 5;
+        const unsigned long long R0 = __builtin_amdgcn_ballot_w64(lvl == 0), R1 = __builtin_amdgcn_ballot_w64(lvl == 1),
+                                 R2 = __builtin_amdgcn_ballot_w64(lvl == 2), R3 = __builtin_amdgcn_ballot_w64(lvl == 3),
+                                 OV = __builtin_amdgcn_ballot_w64(lvl == 4);
+        const int L0 = __popcll(R0), L1 = __popcll(R1), L2 = __popcll(R2), L3 = __popcll(R3);
+        const unsigned long long Rk = lvl == 0 ? R0 : (lvl == 1 ? R1 : (lvl == 2 ? R2 : R3));
+        const int f = lvl == 4 ? lanes_below(OV) : __popcll(OV) + lanes_below(~am);
+        const int F3 = 16 - L3, F32 = F3 + 16 - L2, F321 = F32 + 16 - L1;
+        const int fd = f < F3 ? 48 + L3 + f : (f < F32 ? 32 + L2 + (f - F3) : (f < F321 ? 16 + L1 + (f - F32) : L0 + (f - F321)));
+        dst = lvl < 4 ? 16 * lvl + __popcll(lt & Rk) : fd;
     }
-    const int s = __popcll(lt) + lanes_below(eq);
-    const int a4 = (((s & 3) << 4) | (s >> 2)) << 2;
+    const int a4 = dst << 2;
     const int ri = act ? (d.rem | (newl ? (1 << 30) : 0)) : 0;
     const int ri2 = __builtin_amdgcn_ds_permute(a4, ri);
     d.pos = __builtin_amdgcn_ds_permute(a4, d.pos);
@@ -807,6 +865,9 @@ __device__ __forceinline__ void fwd_body(const KArgs& k) {
     unsigned npair = 0, nseg = 0;
     unsigned long long nsamp = 0;
 
+#ifdef NLOSGR_FXCOUNT
+    unsigned long long fdbg[5] = {0ull, 0ull, 0ull, 0ull, 0ull};   // wave-uniform diagnostics
+#endif
     Drain d;
     d.pos = 0; d.rem = 0; d.t = 0.f; d.ga = 0.f; d.al = 0.f; d.st = 0.f;
     d.sc = 0.f; d.wc = 0.f; d.T = 0.f; d.rbase = 0;
@@ -941,6 +1002,28 @@ __device__ __forceinline__ void fwd_body(const KArgs& k) {
                 nseg += (unsigned)__popcll(__builtin_amdgcn_ballot_w64(act));
                 nsamp += (unsigned)__popcll(__builtin_amdgcn_ballot_w64(win));   // every lane: / 64 on the host
             }
+#ifdef NLOSGR_FXCOUNT
+            if (FX && !BR) {   // diagnostics: bank-pair occupancy of this round's ds_add_u64 groups
+                const unsigned res = (unsigned)((d.pos >> 1) & 15);
+                unsigned long long same = __builtin_amdgcn_ballot_w64(act);
+                for (int b = 0; b < 4; ++b) {
+                    const unsigned long long B = __builtin_amdgcn_ballot_w64((res >> b) & 1u);
+                    same &= ((res >> b) & 1u) ? B : ~B;
+                }
+                const unsigned long long gm = 0xFFFFull << (lane & 48);
+                int cg = act ? __popcll(same & gm) : 0;     // lanes of my group on my bank pair
+                for (int o2 = 1; o2 < 16; o2 <<= 1) cg = max(cg, __shfl_xor(cg, o2));
+                int cw = act ? __popcll(same) : 0;
+                for (int o2 = 1; o2 < 64; o2 <<= 1) cw = max(cw, __shfl_xor(cw, o2));
+                unsigned rm = act ? (1u << res) : 0u;
+                for (int o2 = 1; o2 < 64; o2 <<= 1) rm |= (unsigned)__shfl_xor((int)rm, o2);
+                int sg = 0;
+                for (int g4 = 0; g4 < 4; ++g4) sg += __shfl(cg, 16 * g4);
+                const int na = __popcll(__builtin_amdgcn_ballot_w64(act));
+                fdbg[0] += 1ull; fdbg[1] += (unsigned long long)na; fdbg[2] += (unsigned long long)sg;
+                fdbg[3] += (unsigned long long)__popc(rm); fdbg[4] += (unsigned long long)cw;
+            }
+#endif
             const int remw = win ? d.rem : 0;
             float* hb = hist + (win ? (QUAD ? (d.pos & ~(VW - 1)) : d.pos) : (QUAD ? padq : pad));
             float t = d.t;
@@ -1095,6 +1178,10 @@ __device__ __forceinline__ void fwd_body(const KArgs& k) {
             atomicAdd(k.counts + 2, ns);
         }
     }
+#ifdef NLOSGR_FXCOUNT
+    if (lane == 0)
+        for (int c = 0; c < 5; ++c) atomicAdd(&g_fdbg[c], fdbg[c]);
+#endif
     if (BR) {   // bright segments taken (nlosgr_fx_info)
         if (lane == 0 && nseg) atomicAdd(k.fx_info + 3, (int)nseg);
         return;
@@ -2599,6 +2686,13 @@ extern "C" {
 
 int nlosgr_abi_version(void) { return NLOSGR_ABI_VERSION; }
 
+#ifdef NLOSGR_FXCOUNT
+__attribute__((visibility("default"))) int nlosgr_debug_fx_counts(unsigned long long* out8) {
+    if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_fdbg), 8 * sizeof(unsigned long long)) != hipSuccess) return -1;
+    const unsigned long long zero[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_fdbg), zero, sizeof(zero)) == hipSuccess ? 0 : -1;
+}
+#endif
 #ifdef NLOSGR_BCOUNT
 __attribute__((visibility("default"))) int nlosgr_debug_bwd_counts(unsigned long long* out8) {
     if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_bdbg), 8 * sizeof(unsigned long long)) != hipSuccess) return -1;

@@ -21,6 +21,10 @@
 //   mode 15: ds_add_u64, lane l at word base + (l mod 16) + 16 (l / 16) + 48 (l / 32): groups of 16 distinct
 //            mod 16; lanes l and l + 16 distinct mod 32; lanes l and l + 32 equal mod 64 words
 //   mode 16: ds_add_u64, lane l at word base + 16 l: all 64 lanes on one word residue mod 16 (16-way per group)
+//   mode 17: ds_add_u64, lane l at word base + (l mod 16) + (l / 16): conflict-free within each group, but the
+//            groups' words overlap (lane l of group g and lane l + 1 of group g - 1 share an address)
+//   mode 18: ds_add_u64, lane l at word base + (l mod 16): the 4 groups on the same 16 addresses
+//   mode 19: ds_add_u64, lane l at word base + (l mod 16) + 16 (l / 16) - (l / 16): as 17 with groups 15 words apart
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdint.h>
@@ -55,7 +59,10 @@ __global__ __launch_bounds__(256) void bench(float* out, int seed) {
                         : MODE == 12 ? (lane % 32) + 64 * (lane / 32)
                         : MODE == 13 ? 16 * (lane % 4) + lane / 4
                         : MODE == 14 ? 2 * (lane % 16) + 64 * (lane / 16)
-                        : MODE == 15 ? (lane % 16) + 16 * (lane / 16) + 48 * (lane / 32) : 16 * lane;
+                        : MODE == 15 ? (lane % 16) + 16 * (lane / 16) + 48 * (lane / 32)
+                        : MODE == 17 ? (lane % 16) + (lane / 16)
+                        : MODE == 18 ? (lane % 16)
+                        : MODE == 19 ? (lane % 16) + 15 * (lane / 16) : 16 * lane;
             pos = b + 2 * (w % 256);
         } else if (MODE == 6 || MODE == 9) {
             pos = (int)(__builtin_amdgcn_readfirstlane((st >> 8) % (kBins - 160)) & ~1) + 2 * lane;
@@ -116,7 +123,7 @@ void run(float* d) {
 int main() {
     float* d;
     hipMalloc(&d, kBlocks * 256 * sizeof(float));
-    run<0>(d); run<1>(d); run<2>(d); run<3>(d); run<4>(d); run<5>(d); run<6>(d); run<7>(d); run<8>(d); run<9>(d); run<10>(d); run<11>(d); run<12>(d); run<13>(d); run<14>(d); run<15>(d); run<16>(d);
+    run<0>(d); run<1>(d); run<2>(d); run<3>(d); run<4>(d); run<5>(d); run<6>(d); run<7>(d); run<8>(d); run<9>(d); run<10>(d); run<11>(d); run<12>(d); run<13>(d); run<14>(d); run<15>(d); run<16>(d); run<17>(d); run<18>(d); run<19>(d);
     hipFree(d);
     return 0;
 }
