@@ -291,6 +291,12 @@ constexpr int kSteps = NLOSGR_FSTEPS;     // bins per lane per drain round
 constexpr int kRefill = NLOSGR_REFILL;     // refill once this many lanes are idle (or the queue is final)
 constexpr int kBRefill = NLOSGR_BREFILL;   // backward: same rule
 
+#ifndef NLOSGR_FXPERM
+#define NLOSGR_FXPERM 0   // FX refill permutation (opt-in, see fx_perm)
+#endif
+#ifndef NLOSGR_FXBAL
+#define NLOSGR_FXBAL 1    // with NLOSGR_FXPERM: residue balance at refill (fx_balance)
+#endif
 struct FwdLayout {
     int hist, owner, rayq, wave_stride, total;  // offsets in floats
     // fx: the fixed-point drain needs no claim table and no per-lane pad bins (22.7 KB per C3
@@ -298,7 +304,8 @@ struct FwdLayout {
     __host__ __device__ FwdLayout(int nr, int nt, int np_, bool fx = false) {
         const int off = al4(2 * (nt + np_));  // float2 theta table [nt], float2 phi table [np]
         hist = 0;                             // [nr + kSteps] bins + [kSteps + 64] pad bins (fx: [nr + kSteps + 2])
-        owner = fx ? al4(nr + kSteps + 4) : al4(nr + 2 * kSteps + 64);   // u8 [nr] claim table
+        // fx: the histogram's fields, then 16 residue counters of the refill balance (fx_balance)
+        owner = fx ? al4(nr + kSteps + 4) + (NLOSGR_FXPERM && NLOSGR_FXBAL ? 16 : 0) : al4(nr + 2 * kSteps + 64);   // u8 [nr] claim table
         rayq = owner + (fx ? 0 : al4((nr + 3) / 4));   // uint [kRQ] ring
         wave_stride = al4(rayq + kRQ);
         hist += off; owner += off; rayq += off;
@@ -595,6 +602,49 @@ __device__ __forceinline__ void fx_place(bool newl, bool act, Drain& d) {
     }
 }
 
+// FX refill balance (no-occlusion FX drain, with the deal below).  The deal leaves a group cost of about
+// ceil(c / 4) for a residue held by c segments, so the largest residue count sets the ds_add_u64 conflicts
+// (scripts/fx_counts.py).  At refill each new segment may start up to kFxShift words early (exact Gaussian
+// values before its support, as fx_place): it takes the smallest shift whose residue holds fewer than
+// ceil(active / 16) segments, claimed with a wave-private LDS counter per residue (ds_add_rtn; a claim past
+// the cap is undone and the next shift tried; none free: no shift).  Placement affects only conflicts.
+#ifndef NLOSGR_FXBAL
+#define NLOSGR_FXBAL 1
+#endif
+__device__ __forceinline__ void fx_balance(bool newl, bool act, Drain& d, unsigned* cnt) {
+    const int lane = lane_id();
+    if (lane < 16) cnt[lane] = 0u;
+    wave_sync();
+    const int pb = d.pos >> 1, o = d.pos & 1;
+    if (act && !newl)
+        __hip_atomic_fetch_add(cnt + (pb & 15), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    wave_sync();
+    const unsigned cap = (unsigned)((__popcll(__builtin_amdgcn_ballot_w64(act)) + 15) >> 4);
+    // reach: the seed exponent at the new start stays >= -100 (no flush to zero), the start >= bin 0
+    const float span = d.al + 100.f;
+    const float tm = span > 0.f ? __builtin_amdgcn_sqrtf(span * __builtin_amdgcn_rcpf(fmaxf(-d.ga, 1e-30f))) : 0.f;
+    const int smax = newl ? min(min(kFxShift, pb), (int)floorf(0.5f * (d.t - (float)o + tm))) : -1;
+    int sh = -1;
+#pragma unroll
+    for (int s2 = 0; s2 <= kFxShift; ++s2) {
+        const bool tryit = newl && sh < 0 && s2 <= smax;
+        if (!__builtin_amdgcn_ballot_w64(tryit)) break;
+        if (tryit) {
+            unsigned* c = cnt + ((pb - s2) & 15);
+            const unsigned v = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+            if (v < cap) sh = s2;
+            else __hip_atomic_fetch_add(c, 0xFFFFFFFFu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        }
+    }
+    wave_sync();
+    if (sh > 0) {
+        const int delta = o + 2 * sh;
+        d.pos -= delta;
+        d.rem += delta;
+        d.t -= (float)delta;
+    }
+}
+
 // FX refill permutation (no-occlusion FX drain).  Every active lane advances the same kSteps / 2 words per
 // round, so the bank pair (word mod 16) of each segment relative to the others is fixed for its life: the
 // conflicts of a ds_add_u64 (serviced in 4 groups of 16 lanes, bank pair = word mod 16; scripts/lds_fx_probe.hip
@@ -611,72 +661,20 @@ __device__ __forceinline__ void fx_place(bool newl, bool act, Drain& d) {
 #define NLOSGR_FXPERM 0
 #endif
 constexpr bool kFxPerm = NLOSGR_FXPERM != 0;
-constexpr int kFxPermMode = NLOSGR_FXPERM;   // 1: deal, 2: levels
 __device__ __forceinline__ void fx_perm(bool& newl, bool& act, Drain& d, float& fpk) {
     const unsigned res = (unsigned)((d.pos >> 1) & 15);
-    const unsigned long long am = __builtin_amdgcn_ballot_w64(act);
-    int dst;
-    if (kFxPermMode == 1) {
-        // deal: sorted by (residue, lane), idle lanes last; position s -> lane 16 (s mod 4) + s / 4
-        const unsigned key = act ? res : 16u;
-        unsigned long long eq = ~0ull, lt = 0ull;
+    // deal: sorted by (residue, lane), idle lanes last; position s -> lane 16 (s mod 4) + s / 4
+    const unsigned key = act ? res : 16u;
+    unsigned long long eq = ~0ull, lt = 0ull;
 #pragma unroll
-        for (int b = 4; b >= 0; --b) {
-            const bool mine = (key >> b) & 1u;
-            const unsigned long long B = __builtin_amdgcn_ballot_w64(mine);
-            lt |= mine ? (eq & ~B) : 0ull;
-            eq &= mine ? B : ~B;
-        }
-        const int s = __popcll(lt) + lanes_below(eq);
-        dst = ((s & 3) << 4) | (s >> 2);
-    } else if (kFxPermMode == 3) {
-        // rank mod 4: the segment of rank j among its residue's goes to group j mod 4 (a residue held by c
-        // segments costs ceil((c - g) / 4) in group g: the sum over groups is the largest c, the least any
-        // assignment reaches); a group past 16 lanes spills its last lanes, then the idle lanes, into the
-        // other groups' free slots (group 3 first)
-        unsigned long long eq = am;
-#pragma unroll
-        for (int b = 3; b >= 0; --b) {
-            const bool mine = (res >> b) & 1u;
-            const unsigned long long B = __builtin_amdgcn_ballot_w64(mine);
-            eq &= mine ? B : ~B;
-        }
-        const int g = act ? (lanes_below(eq) & 3) : 4;
-        const unsigned long long G0 = __builtin_amdgcn_ballot_w64(g == 0), G1 = __builtin_amdgcn_ballot_w64(g == 1),
-                                 G2 = __builtin_amdgcn_ballot_w64(g == 2), G3 = __builtin_amdgcn_ballot_w64(g == 3);
-        const int N0 = min(__popcll(G0), 16), N1 = min(__popcll(G1), 16), N2 = min(__popcll(G2), 16),
-                  N3 = min(__popcll(G3), 16);
-        const unsigned long long Gk = g == 0 ? G0 : (g == 1 ? G1 : (g == 2 ? G2 : G3));
-        const int ig = lanes_below(Gk);
-        const bool spill = g == 4 || ig >= 16;
-        const unsigned long long SP = __builtin_amdgcn_ballot_w64(spill && g < 4);
-        const int f = g < 4 ? lanes_below(SP) : __popcll(SP) + lanes_below(~am);
-        const int F3 = 16 - N3, F32 = F3 + 16 - N2, F321 = F32 + 16 - N1;
-        const int fd = f < F3 ? 48 + N3 + f : (f < F32 ? 32 + N2 + (f - F3) : (f < F321 ? 16 + N1 + (f - F32) : N0 + (f - F321)));
-        dst = spill ? fd : 16 * g + ig;
-    } else {
-        // levels: the segment of rank k among its residue's (k < 4) goes to group k, at the index of its
-        // residue among that level's (one segment per residue: conflict-free); ranks >= 4 and then the
-        // idle lanes fill the groups' remaining slots, group 3 first
-        unsigned long long eq = am, lt = 0ull;
-#pragma unroll
-        for (int b = 3; b >= 0; --b) {
-            const bool mine = (res >> b) & 1u;
-            const unsigned long long B = __builtin_amdgcn_ballot_w64(mine);
-            lt |= mine ? (eq & ~B) : 0ull;
-            eq &= mine ? B : ~B;
-        }
-        const int lvl = act ? min(lanes_below(eq), 4) : 5;
-        const unsigned long long R0 = __builtin_amdgcn_ballot_w64(lvl == 0), R1 = __builtin_amdgcn_ballot_w64(lvl == 1),
-                                 R2 = __builtin_amdgcn_ballot_w64(lvl == 2), R3 = __builtin_amdgcn_ballot_w64(lvl == 3),
-                                 OV = __builtin_amdgcn_ballot_w64(lvl == 4);
-        const int L0 = __popcll(R0), L1 = __popcll(R1), L2 = __popcll(R2), L3 = __popcll(R3);
-        const unsigned long long Rk = lvl == 0 ? R0 : (lvl == 1 ? R1 : (lvl == 2 ? R2 : R3));
-        const int f = lvl == 4 ? lanes_below(OV) : __popcll(OV) + lanes_below(~am);
-        const int F3 = 16 - L3, F32 = F3 + 16 - L2, F321 = F32 + 16 - L1;
-        const int fd = f < F3 ? 48 + L3 + f : (f < F32 ? 32 + L2 + (f - F3) : (f < F321 ? 16 + L1 + (f - F32) : L0 + (f - F321)));
-        dst = lvl < 4 ? 16 * lvl + __popcll(lt & Rk) : fd;
+    for (int b = 4; b >= 0; --b) {
+        const bool mine = (key >> b) & 1u;
+        const unsigned long long B = __builtin_amdgcn_ballot_w64(mine);
+        lt |= mine ? (eq & ~B) : 0ull;
+        eq &= mine ? B : ~B;
     }
+    const int s = __popcll(lt) + lanes_below(eq);
+    const int dst = ((s & 3) << 4) | (s >> 2);
     const int a4 = dst << 2;
     const int ri = act ? (d.rem | (newl ? (1 << 30) : 0)) : 0;
     const int ri2 = __builtin_amdgcn_ds_permute(a4, ri);
@@ -956,8 +954,11 @@ __device__ __forceinline__ void fwd_body(const KArgs& k) {
                 qcount -= ntake;
                 // (netf keeps its start: its transmittance would have to be re-seeded)
                 bool newl = take && act;
+                if (FX && !BR && NLOSGR_FXBAL && kFxPerm && kFxShift > 0 && MODE == NLOSGR_MODE_NOOCL)
+                    fx_balance(newl, act, d, reinterpret_cast<unsigned*>(hist + al4(nr + kSteps + 4)));
                 if (FX && !BR && kFxPerm && MODE == NLOSGR_MODE_NOOCL) fx_perm(newl, act, d, fpk);
-                if (FX && !BR && kFxShift > 0 && MODE != NLOSGR_MODE_NETF) fx_place(newl, act, d);
+                if (FX && !BR && kFxShift > 0 && MODE != NLOSGR_MODE_NETF && !(NLOSGR_FXBAL && kFxPerm && MODE == NLOSGR_MODE_NOOCL))
+                    fx_place(newl, act, d);
             }
             const bool anyact = __builtin_amdgcn_ballot_w64(act) != 0;
             if (!anyact) {
