@@ -25,8 +25,8 @@ else:
 f = features_flat(m).detach()
 args = (m._mu.detach(), m._scaling.detach(), m._rotation.detach(), m._opacity.detach(), f, geo)
 if os.environ.get('NLOSGR_ABLATE_ORDER') == 'slab':   # the Gaussian order TrainStep hands the backward
-    from nlosgr.train import slab_order
-    perm = slab_order(args[0], geo.wall, size=args[1].max(1).values)
+    from nlosgr.train import slab_order, wall_centroid
+    perm = slab_order(args[0], None, 8, 4, size=args[1].max(1).values, centroid=wall_centroid(geo.wall))
     args = tuple(t[perm].contiguous() for t in args[:5]) + (geo,)
 base = make_config(m, scene, preset, mode, cutoff=cutoff)
 res = {}
@@ -39,7 +39,10 @@ if os.environ.get("NLOSGR_ABLATE_FWD_ONLY") == "1":
     print(json.dumps({'config': cfgname, 'mode': mode, 'cutoff': cutoff, 'fwd_ms_by_flags': res}))
     sys.exit(0)
 cache = os.environ.get("NLOSGR_ABLATE_CACHE", "1") == "1"
-hist, _, ws = render_forward(*args, base, ray_cache=True)
+if cache:
+    hist, _, ws = render_forward(*args, base, ray_cache=True)
+else:
+    hist, _ = render_forward(*args, base)
 grad = torch.randn_like(hist) * 1e-3
 bres = {}
 for flags in (0, 64, 32, 4, 1, 2):

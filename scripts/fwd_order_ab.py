@@ -30,7 +30,12 @@ orders = {'given': None,
           'size': slab_order(P[0], geo.wall, 1, 1, size=size),
           'slab8x1': slab_order(P[0], geo.wall, 8, 1),
           'slab4x2_size': slab_order(P[0], geo.wall, 4, 2, size=size),
-          'slab32x1_size': slab_order(P[0], geo.wall, 32, 1, size=size)}
+          'slab32x1_size': slab_order(P[0], geo.wall, 32, 1, size=size),
+          'slab8x1_sizedesc': slab_order(P[0], geo.wall, 8, 1, size=-size),
+          'slab4x1_size': slab_order(P[0], geo.wall, 4, 1, size=size),
+          'slab2x1_size': slab_order(P[0], geo.wall, 2, 1, size=size),
+          'slab64x1': slab_order(P[0], geo.wall, 64, 1),
+          'slab8x2_size': slab_order(P[0], geo.wall, 8, 2, size=size)}
 args = {k: (P if o is None else [t[o].contiguous() for t in P]) for k, o in orders.items()}
 times = {k: [] for k in orders}
 ref = None
