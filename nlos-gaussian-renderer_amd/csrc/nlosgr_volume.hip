@@ -489,7 +489,9 @@ constexpr float kBetaSeries = 0.5f;   // bin-integrated TAIL drain: series bin a
 // peak is >= 2^kFxBits units at refill ("bright"; at most the segments of the ceil(ng/256) Gaussians above
 // the quantile, and none unless the bounds spread by more than the C-S slack) bypasses the LDS: its lane
 // adds its values as u64 integers straight into the wall point's global u64 row (agent-scope atomics), so
-// it is as exact as the rest.  E is clamped to <= E(max bound) + kFxRange so those u64 sums cannot wrap.
+// it is as exact as the rest.  E is clamped to <= E(max bound) + range, range = kFxRange or less when
+// (bright Gaussians <= ceil(ng / 256)) x (rays per wall point) bright terms per bin could pass 2^(63 - kFxBits -
+// range): the u64 sums cannot wrap (C3 / C5: range 16, at most 2^19 / 2^21 bright terms of < 2^40 units).
 // A low word must never carry into its high word: every lane sums the peaks (exp2 of the segment's log2
 // amplitude, in units) of the LDS segments it took since the last check; a segment adds at most its peak
 // to any bin once, so while every lane's sum stays <= thr the largest field stays <= M + 64 thr < 2^32.
@@ -501,7 +503,7 @@ constexpr float kBetaSeries = 0.5f;   // bin-integrated TAIL drain: series bin a
 __device__ unsigned long long g_fdbg[8];
 #endif
 constexpr int kFxBits = 24;
-constexpr int kFxRange = 20;                 // E <= E(max bound) + kFxRange: u64 terms < 2^(kFxBits + kFxRange)
+constexpr int kFxRange = 16;                 // E <= E(max bound) + kFxRange: u64 terms < 2^(kFxBits + kFxRange)
 constexpr float kFxBright = 16777216.0f;     // 2^kFxBits
 constexpr float kFxMargin = 1.002f;          // segment peak <= bound x 2^E x kFxMargin (binint 1.001, netf (1+1e-7)^nr)
 constexpr float kFxLimit = 4294967040.0f;   // largest float below 2^32
@@ -1276,7 +1278,8 @@ __global__ __launch_bounds__(kBlock) void fx_bound_kernel(nlosgr_gaussians g, fl
 // least ceil(n / 256) counted bounds at or above it (bin e holds bounds in [2^(e-127), 2^(e-126))), so
 // fewer than ceil(n / 256) Gaussians have a bound above 2^(e_q - 126); E = kFxBits - (e_q - 126) puts that
 // bound below 2^kFxBits units.  E <= E(top bin) + kFxRange.  info[0] = E, info[1] = E of the top bin.
-__global__ __launch_bounds__(kFxBins) void fx_unit_kernel(const unsigned* __restrict__ bins, int* info, int maxunit) {
+__global__ __launch_bounds__(kFxBins) void fx_unit_kernel(const unsigned* __restrict__ bins, int* info, int maxunit,
+                                                         int range) {
     __shared__ unsigned cum[kFxBins];
     const int t = threadIdx.x;
     cum[t] = bins[t];
@@ -1302,7 +1305,7 @@ __global__ __launch_bounds__(kFxBins) void fx_unit_kernel(const unsigned* __rest
         auto unit = [](int e) { const int u = kFxBits - (e - 126); return u < -120 ? -120 : (u > 120 ? 120 : u); };
         const int emax = n > 0u ? unit(et) : 0;
         int e = n > 0u ? unit(maxunit ? et : eq) : 0;   // maxunit: round 5's rule (diagnostics)
-        if (e > emax + kFxRange) e = emax + kFxRange;
+        if (e > emax + range) e = emax + range;
         info[0] = e;
         info[1] = emax;
     }
@@ -2610,8 +2613,18 @@ int run_fwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosgr_
         else
             hipLaunchKernelGGL(fx_bound_kernel<NLOSGR_PRESET_CUDA>, dim3(nb), dim3(kBlock), 0, s, *g, ascale, bins, bound);
         HIPCHK(hipGetLastError());
+        // E <= E(max) + range: a bright term < 2^(kFxBits + range) units, and a bin receives at most
+        // ceil(ng / 256) x nt x np bright terms per wall point, so its u64 sum stays below 2^63
+        int range = kFxRange;
+        {
+            const double nterm = (double)((g->ng + 255) / 256) * (double)geo->nt * (double)geo->np;
+            int bits = 0;
+            while (bits < 63 && ldexp(1.0, bits) < nterm) ++bits;
+            range = 63 - kFxBits - bits;
+            range = range < 0 ? 0 : (range > kFxRange ? kFxRange : range);
+        }
         hipLaunchKernelGGL(fx_unit_kernel, dim3(1), dim3(kFxBins), 0, s, bins, ka.fx_info,
-                           (opt->flags & NLOSGR_FLAG_FX_MAXUNIT) ? 1 : 0);
+                           (opt->flags & NLOSGR_FLAG_FX_MAXUNIT) ? 1 : 0, range);
         HIPCHK(hipGetLastError());
         hipLaunchKernelGGL(fx_blist_kernel, dim3(nb), dim3(kBlock), 0, s, bound, g->ng, ka.fx_info, blist);
         HIPCHK(hipGetLastError());

@@ -221,3 +221,28 @@ def test_fx_nan_gaussian_is_skipped():
     err = float((a - b).abs().max() / b.abs().max())
     print(f"\nNaN Gaussian: E {info[0]}, vs without it {err:.3e} of max")
     assert err <= 1e-6
+
+
+def test_fx_unit_range_clamp():
+    """Bright Gaussians ~1e7x above the quantile's bound: the unit is clamped to 16 binary orders below the
+    largest bound's (so the bright launch's u64 sums cannot wrap: a bright term < 2^40 units), and the whole
+    volume still matches the float64 sum of fp32 sub-histograms to 2e-5 of each row's max."""
+    from nlosgr import GaussianParams
+    from nlosgr.volume import Scene, make_config
+    dev = torch.device("cuda:0")
+    ng = 8000
+    scene = Scene(H=4, W=4, T=256, ns=16)
+    m = GaussianParams.synthetic(ng, 3, preset="cuda", device=dev, seed=12)
+    bidx = torch.arange(5, ng, 800, device=dev)
+    _bright(m, bidx, rho=2e6)
+    P = _params(m)
+    geo = scene.geometry(dev, "cuda", "noocl")
+    cfg = make_config(m, scene, "cuda", "noocl", cutoff=CUT)
+    ref = _chunk_sum(P, geo, cfg)
+    a, info = _fx(P, geo, cfg)
+    row = ((a - ref).abs().max(1).values / ref.abs().max(1).values)
+    print(f"\nrange clamp: E {info[0]} (max-bound E {info[1]}), bright segments {info[3]}, "
+          f"row err / row max {float(row.max()):.3e}")
+    assert info[0] == info[1] + 16, info
+    assert info[3] > 0
+    assert float(row.max()) <= 2e-5
