@@ -663,6 +663,11 @@ __device__ __forceinline__ void fx_balance(bool newl, bool act, Drain& d, unsign
 #define NLOSGR_FXPERM 0
 #endif
 constexpr bool kFxPerm = NLOSGR_FXPERM != 0;
+#ifndef NLOSGR_FXPERM_NETF
+#define NLOSGR_FXPERM_NETF 0   // measured: netf fwd 894.5 vs 884.5 ms without (its drain is less LDS-bound)
+#endif
+constexpr bool kFxPermNetf = NLOSGR_FXPERM_NETF != 0;
+template <int MODE>
 __device__ __forceinline__ void fx_perm(bool& newl, bool& act, Drain& d, float& fpk) {
     const unsigned res = (unsigned)((d.pos >> 1) & 15);
     // deal: sorted by (residue, lane), idle lanes last; position s -> lane 16 (s mod 4) + s / 4
@@ -685,6 +690,10 @@ __device__ __forceinline__ void fx_perm(bool& newl, bool& act, Drain& d, float& 
     d.ga = __int_as_float(__builtin_amdgcn_ds_permute(a4, __float_as_int(d.ga)));
     d.al = __int_as_float(__builtin_amdgcn_ds_permute(a4, __float_as_int(d.al)));
     fpk = __int_as_float(__builtin_amdgcn_ds_permute(a4, __float_as_int(fpk)));
+    if (MODE == NLOSGR_MODE_NETF) {   // the segment's transmittance (carrying its weight) and sigma c dT
+        d.T = __int_as_float(__builtin_amdgcn_ds_permute(a4, __float_as_int(d.T)));
+        d.sc = __int_as_float(__builtin_amdgcn_ds_permute(a4, __float_as_int(d.sc)));
+    }
     act = ri2 != 0;
     newl = (ri2 >> 30) & 1;
     d.rem = ri2 & ((1 << 30) - 1);
@@ -958,7 +967,10 @@ __device__ __forceinline__ void fwd_body(const KArgs& k) {
                 bool newl = take && act;
                 if (FX && !BR && NLOSGR_FXBAL && kFxPerm && kFxShift > 0 && MODE == NLOSGR_MODE_NOOCL)
                     fx_balance(newl, act, d, reinterpret_cast<unsigned*>(hist + al4(nr + kSteps + 4)));
-                if (FX && !BR && kFxPerm && MODE == NLOSGR_MODE_NOOCL) fx_perm(newl, act, d, fpk);
+                // netf has no refill placement (its transmittance would need re-seeding); the deal is opt-in
+                // there too (NLOSGR_FXPERM_NETF)
+                if (FX && !BR && ((kFxPerm && MODE == NLOSGR_MODE_NOOCL) || (kFxPermNetf && MODE == NLOSGR_MODE_NETF)))
+                    fx_perm<MODE>(newl, act, d, fpk);
                 if (FX && !BR && kFxShift > 0 && MODE != NLOSGR_MODE_NETF && !(NLOSGR_FXBAL && kFxPerm && MODE == NLOSGR_MODE_NOOCL))
                     fx_place(newl, act, d);
             }
