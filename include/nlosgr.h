@@ -123,7 +123,8 @@ typedef struct {
                                  Culled (cutoff > 0), histogram-only calls.  In NLOSGR_MODE_OCCL it is
                                  the row cache instead: the forward stores every ray tile's (D, W) rows
                                  (8 B per wall point x ray x bin; C3 128 GiB) and the backward on the
-                                 same workspace reloads them instead of re-running its forward sweep.
+                                 same workspace reloads them instead of re-running its forward sweep
+                                 (and, when the forward was one wall-point launch, its tile bins).
                                  0 = off */
     int32_t selection;        /* NLOSGR_SELECT_*.  OCCL mode and AABB selection run the ray-tile engine
                                  (ray-major, per-ray compositing, deterministic); the ray cache and

@@ -1424,8 +1424,13 @@ int tiles_bwd(const nlosgr_gaussians* g, const nlosgr_geometry* geo, const nlosg
             TArgs b = batch_args(a, P, geo, p0, pn);
             b.grad_hist = grad_hist ? grad_hist + (size_t)p0 * nr : nullptr;
             b.grad_ray = grad_ray ? grad_ray + (size_t)p0 * nt * np_ * nr : nullptr;
-            rc = bin_batch(b, P, s);
-            if (rc) return rc;
+            // with the row cache the workspace holds the forward of these inputs (the rows the backward
+            // reloads); when that forward was one launch (one wall-point batch), its tile cones and bins are
+            // this batch's too and are not rebuilt
+            if (!(a.rcache && P.pbatch >= geo->nwall)) {
+                rc = bin_batch(b, P, s);
+                if (rc) return rc;
+            }
             dispatch_tile<true>(b, shm, s);
             HIPCHK(hipGetLastError());
         }
