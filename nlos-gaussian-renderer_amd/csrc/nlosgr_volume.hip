@@ -1680,6 +1680,10 @@ __device__ __forceinline__ bool bray_setup(const float* pd, float2 th, float2 ph
 #define NLOSGR_SHAPE_SENDER 1
 #endif
 constexpr bool kShapeSender = NLOSGR_SHAPE_SENDER;   // see rD / rK in bwd_kernel
+#ifndef NLOSGR_NETF_CLOSED
+#define NLOSGR_NETF_CLOSED 1
+#endif
+constexpr bool kNetfClosed = NLOSGR_NETF_CLOSED;     // netf TAIL backward: part B set at the ray start (bwd_kernel)
 
 // TAIL (culled no-occlusion histogram backward at cutoff >= kTailCutoff): the drain reads the upstream
 // row without the segment-end mask, see BV below
@@ -1864,6 +1868,36 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_B
                     act = bray_setup<MODE, DENSE>(pdat, tth[i], tph[j], slot, i, j, nr, mc2, r0, dr,
                                                   inv_dr, f0log2, b) && !(k.opt.flags & 4);  // flags 4: no bins
                     if (MODE == NLOSGR_MODE_NETF && TAIL) b.T *= b.st;   // sin(theta) rides on T (BV rows)
+                    if (MODE == NLOSGR_MODE_NETF && TAIL && !DENSE && kNetfClosed && act) {
+                        // part B's sums are a_c sigma sum_j pdf_j (1, kap_j, kap_j^2) over the ray's bins, which the
+                        // TAIL rounds cover to past 5 sigma on both sides: they are set here once instead of 3 VALU
+                        // per bin.  A ray at least one bin wide (sigma_b^2 = 1 / (a dr^2) >= 1) whose Gaussian lies
+                        // inside the histogram by 6 sigma_b on both sides: its own moments 2^c0 sqrt(2 pi) sigma_b
+                        // (1, 0, sigma_b^2) (Poisson summation: relative error <= exp(-2 pi^2 sigma_b^2) < 3e-9, plus
+                        // the tails past 5 sigma the rounds leave out, < 3e-7 of the ray's sum); any other (narrow, or
+                        // cut by the first or last bin): its support bins [kl, kh] summed here
+                        const float sb2 = kHalfLog2e * frcp(-b.c2);
+                        const float ksb = (float)b.kl - b.kap0;   // the closest approach, in bins
+                        const float w6 = 6.0f * __builtin_amdgcn_sqrtf(sb2);
+                        float g0 = 0.f, g1 = 0.f, g2 = 0.f;
+                        if (sb2 >= 1.0f && ksb - w6 >= 0.f && ksb + w6 <= (float)(nr - 1)) {
+                            g0 = fast_exp2(b.c0) * (2.50662827463f * __builtin_amdgcn_sqrtf(sb2));
+                            g2 = g0 * sb2;
+                        } else {
+                            for (int jb = b.kl; jb < b.kl + b.len; ++jb) {
+                                const float kj = b.kap0 + (float)(jb - b.kl);
+                                const float pj = fast_exp2(fmaf(b.c2, kj * kj, b.c0));
+                                g0 += pj;
+                                g1 = fmaf(pj, kj, g1);
+                                g2 = fmaf(pj * kj, kj, g2);
+                            }
+                        }
+                        const float acl = -cdt / (1.0f + 1e-7f);
+                        b.S0b = b.sigma * acl * g0;
+                        b.S1b = b.sigma * acl * g1;
+                        b.S2b = b.sigma * acl * g2;
+                        b.dsigb = acl * g0;
+                    }
                 }
                 const int ntake = min(nidle, qcount);
                 BDBG(6, 1); BDBG(7, ntake);
@@ -2038,6 +2072,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_B
                         // part A's moments by nested running sums (as the no-occlusion drain): UA0 = sum hA,
                         // UA1 = sum hA w, UA2 = sum hA w (w + 1) / 2 with w = kRS - m; part B's directly
                         float UA0 = 0.f, UA1 = 0.f, UA2 = 0.f, UB0 = 0.f, UB1 = 0.f, UB2 = 0.f;
+                        constexpr bool UB = !(TAIL && kNetfClosed);   // part B per bin (else set at the ray's start)
 #pragma unroll
                         for (int m = 0; m < kRS; ++m) {
                             // TAIL: no segment-end mask (the bins past the end carry the Gaussian's exact
@@ -2051,20 +2086,23 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NLOSGR_B
                             const float HT = Hs[m] * T;
                             drho = fmaf(HT, pdf, drho);               // D
                             const float c1 = in ? fmaf(kk, drho, HT) : 0.f;
-                            const float pin = in ? pdf : 0.f;
                             UA0 = fmaf(c1, pdf, UA0);                 // x crho sigma at the end
                             UA1 += UA0;
                             UA2 += UA1;
-                            UB0 += pin;
-                            UB1 = fmaf(pin, (float)m, UB1);
-                            UB2 = fmaf(pin, (float)(m * m), UB2);
+                            if (UB) {
+                                const float pin = in ? pdf : 0.f;
+                                UB0 += pin;
+                                UB1 = fmaf(pin, (float)m, UB1);
+                                UB2 = fmaf(pin, (float)(m * m), UB2);
+                            }
                             T *= in ? f : 1.f;
                         }
                         dsig = fmaf(crho, UA0, dsig);
                         pre = b.rho * sx * drho;
                         // S_n += sum h (kb + m)^n, kb = the round's first bin offset
                         const float kb = kseed;
-                        const float sg = b.sigma * crho, sgb = b.sigma * ac;
+                        const float sg = b.sigma * crho;
+                        const float sgb = b.sigma * ac;
                         const float KA = kb + (float)kRS;   // kap at slot kRS
                         S0 = fmaf(sg, UA0, S0);
                         S1 = fmaf(sg, fmaf(KA, UA0, -UA1), S1);
