@@ -92,6 +92,11 @@ constexpr int kWalkC0 = 96, kWalkC1 = 56, kWalkC2 = 28;   // walk-length class b
 #ifndef NLOSGR_WALK_UNROLL
 #define NLOSGR_WALK_UNROLL 4
 #endif
+#ifndef NLOSGR_WALK_RESEED
+#define NLOSGR_WALK_RESEED 16   // backward pair walks: exp2 recurrence re-seeded every this many bins (0: exp2 per bin)
+#endif
+constexpr int kWalkReseed = NLOSGR_WALK_RESEED;
+static_assert((kWalkReseed & (kWalkReseed - 1)) == 0, "the re-seed period is a power of two");
 #ifndef NLOSGR_WALK_REC
 #define NLOSGR_WALK_REC 1
 #endif
@@ -868,6 +873,31 @@ __global__ __launch_bounds__(tile_threads<BWD>()) void tile_kernel(TArgs k) {
                                         m1 = fmaf(G, t, m1);
                                         m2 = fmaf(G * t, t, m2);
                                     };
+                                    if (kWalkReseed > 0) {
+                                        // pdf by the exp2 recurrence (pdf(t + 1) = pdf(t) q, q(t + 1) = q(t) 2^(2 ga)),
+                                        // re-seeded with exact exp2 every kWalkReseed bins of the walk: every lane
+                                        // starts its walk together, so the re-seed is uniform across the wave
+                                        // (round 5's re-seed at absolute bin multiples made some lane re-seed
+                                        // almost every step).  Inside the support at m_c^2 <= 36 the ratio's
+                                        // exponent stays below 27 (no overflow); error <= kWalkReseed^2 / 4 ulp
+                                        const float cc = fast_exp2(2.f * ga);
+                                        float pc = 0.f, qc = 0.f;
+                                        int it = 0;
+#pragma unroll NLOSGR_WALK_UNROLL
+                                        for (int kb = kl; kb <= kh; ++kb, tt += 1.f, ++it) {
+                                            if ((it & (kWalkReseed - 1)) == 0) {
+                                                pc = fast_exp2(fmaf(ga, tt * tt, al));
+                                                qc = fast_exp2(ga * fmaf(2.f, tt, 1.f));
+                                            }
+                                            const float pdf = pc;
+                                            pc *= qc;
+                                            qc *= cc;
+                                            const float2 ab = ab0;
+                                            ab0 = ab1;
+                                            ab1 = row[kb + 2];
+                                            bin(pdf, ab, tt);
+                                        }
+                                    } else {
 #pragma unroll NLOSGR_WALK_UNROLL
                                     for (int kb = kl; kb <= kh; ++kb, tt += 1.f) {
                                         const float pdf = fast_exp2(fmaf(ga, tt * tt, al));
@@ -875,6 +905,7 @@ __global__ __launch_bounds__(tile_threads<BWD>()) void tile_kernel(TArgs k) {
                                         ab0 = ab1;
                                         ab1 = row[kb + 2];
                                         bin(pdf, ab, tt);
+                                    }
                                     }
                                     ps = m0;
                                     m0 *= wsg;
