@@ -92,10 +92,6 @@ constexpr int kWalkC0 = 96, kWalkC1 = 56, kWalkC2 = 28;   // walk-length class b
 #ifndef NLOSGR_WALK_UNROLL
 #define NLOSGR_WALK_UNROLL 4
 #endif
-#ifndef NLOSGR_ENTRY_PREFETCH
-#define NLOSGR_ENTRY_PREFETCH 0   // forward entry loop: the next entry's reads before this entry's math
-#endif
-constexpr bool kEntryPrefetch = NLOSGR_ENTRY_PREFETCH;
 #ifndef NLOSGR_WALK_RESEED
 #define NLOSGR_WALK_RESEED 16   // backward pair walks: exp2 recurrence re-seeded every this many bins (0: exp2 per bin)
 #endif
@@ -663,7 +659,11 @@ __global__ __launch_bounds__(tile_threads<BWD>()) void tile_kernel(TArgs k) {
                                         // chunk instead of both forms per entry; C3 occl AABB forward 1341 -> 1260 ms)
                                         auto entries = [&](auto smallc) {
                                             constexpr bool kSmall = decltype(smallc)::value;
-                                            auto one = [&](const float4 e0, const float4 e1) {
+                                            while (cm) {
+                                                const int s = __builtin_ctzll(cm);
+                                                cm &= cm - 1;
+                                                const int idx = __popcll(pm & ((1ull << s) - 1ull));
+                                                const float4 e0 = el[2 * idx], e1 = el[2 * idx + 1];
                                                 const int skl = __float_as_int(e1.y), slen = __float_as_int(e1.z);   // kh - kl
                                                 const float tt = kf - e0.x;
                                                 const float pdf = fast_exp2(fmaf(e0.y, tt * tt, e0.z));
@@ -682,36 +682,6 @@ __global__ __launch_bounds__(tile_threads<BWD>()) void tile_kernel(TArgs k) {
                                                     accW = fmaf(e1.x, w, accW);
                                                 } else {
                                                     accW = fmaf(e1.x, cv, accW);
-                                                }
-                                            };
-                                            if (kEntryPrefetch) {
-                                                // the next entry's (uniform-address) reads issue before this entry's math
-                                                if (!cm) return;
-                                                int s = __builtin_ctzll(cm);
-                                                cm &= cm - 1;
-                                                int idx = __popcll(pm & ((1ull << s) - 1ull));
-                                                float4 e0 = el[2 * idx], e1 = el[2 * idx + 1];
-                                                while (true) {
-                                                    const bool more = cm != 0;
-                                                    float4 n0 = e0, n1 = e1;
-                                                    if (more) {
-                                                        s = __builtin_ctzll(cm);
-                                                        cm &= cm - 1;
-                                                        idx = __popcll(pm & ((1ull << s) - 1ull));
-                                                        n0 = el[2 * idx];
-                                                        n1 = el[2 * idx + 1];
-                                                    }
-                                                    one(e0, e1);
-                                                    if (!more) break;
-                                                    e0 = n0;
-                                                    e1 = n1;
-                                                }
-                                            } else {
-                                                while (cm) {
-                                                    const int s = __builtin_ctzll(cm);
-                                                    cm &= cm - 1;
-                                                    const int idx = __popcll(pm & ((1ull << s) - 1ull));
-                                                    one(el[2 * idx], el[2 * idx + 1]);
                                                 }
                                             }
                                         };
