@@ -292,10 +292,10 @@ constexpr int kRefill = NLOSGR_REFILL;     // refill once this many lanes are id
 constexpr int kBRefill = NLOSGR_BREFILL;   // backward: same rule
 
 #ifndef NLOSGR_FXPERM
-#define NLOSGR_FXPERM 0   // FX refill permutation (opt-in, see fx_perm)
+#define NLOSGR_FXPERM 1   // FX refill permutation (the deal, see fx_perm): with the bank placement 745.7 vs 750.6 ms
 #endif
 #ifndef NLOSGR_FXBAL
-#define NLOSGR_FXBAL 1    // with NLOSGR_FXPERM: residue balance at refill (fx_balance)
+#define NLOSGR_FXBAL 0    // with NLOSGR_FXPERM: residue balance at refill instead of the placement (fx_balance, opt-in)
 #endif
 struct FwdLayout {
     int hist, owner, rayq, wave_stride, total;  // offsets in floats
@@ -610,9 +610,6 @@ __device__ __forceinline__ void fx_place(bool newl, bool act, Drain& d) {
 // values before its support, as fx_place): it takes the smallest shift whose residue holds fewer than
 // ceil(active / 16) segments, claimed with a wave-private LDS counter per residue (ds_add_rtn; a claim past
 // the cap is undone and the next shift tried; none free: no shift).  Placement affects only conflicts.
-#ifndef NLOSGR_FXBAL
-#define NLOSGR_FXBAL 1
-#endif
 __device__ __forceinline__ void fx_balance(bool newl, bool act, Drain& d, unsigned* cnt) {
     const int lane = lane_id();
     if (lane < 16) cnt[lane] = 0u;
@@ -659,10 +656,7 @@ __device__ __forceinline__ void fx_balance(bool newl, bool act, Drain& d, unsign
 #ifndef NLOSGR_FX_DIAG_NOCONFLICT
 #define NLOSGR_FX_DIAG_NOCONFLICT 0
 #endif
-#ifndef NLOSGR_FXPERM
-#define NLOSGR_FXPERM 0
-#endif
-constexpr bool kFxPerm = NLOSGR_FXPERM != 0;
+constexpr bool kFxPerm = NLOSGR_FXPERM != 0;   // (defaults with FwdLayout above)
 #ifndef NLOSGR_FXPERM_NETF
 #define NLOSGR_FXPERM_NETF 0   // measured: netf fwd 894.5 vs 884.5 ms without (its drain is less LDS-bound)
 #endif
