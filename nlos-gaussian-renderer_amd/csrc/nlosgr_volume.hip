@@ -289,6 +289,10 @@ constexpr int kSteps = NLOSGR_FSTEPS;     // bins per lane per drain round
 #define NLOSGR_BREFILL 16
 #endif
 constexpr int kRefill = NLOSGR_REFILL;     // refill once this many lanes are idle (or the queue is final)
+#ifndef NLOSGR_REFILL_FX
+#define NLOSGR_REFILL_FX 56
+#endif
+constexpr int kRefillFx = NLOSGR_REFILL_FX;   // the no-occlusion FX drain with the refill deal
 constexpr int kBRefill = NLOSGR_BREFILL;   // backward: same rule
 
 #ifndef NLOSGR_FXPERM
@@ -923,7 +927,10 @@ __device__ __forceinline__ void fwd_body(const KArgs& k) {
             const bool anymore = __builtin_amdgcn_ballot_w64(more) != 0;
             const unsigned long long idle = __builtin_amdgcn_ballot_w64(!act);
             const int nidle = __popcll(idle);
-            if (qcount > 0 && (nidle >= kRefill || !anymore)) {
+            // the no-occlusion FX drain refills later: the deal's cost is per refill (REFILL 48 / 52 / 56 / 60 / 62:
+            // 745.9 / 735.7 / 732.4 / 736.7 / 745.4 ms, same box)
+            constexpr int kRef = (FX && !BR && kFxPerm && MODE == NLOSGR_MODE_NOOCL) ? kRefillFx : kRefill;
+            if (qcount > 0 && (nidle >= kRef || !anymore)) {
                 // idle lane of rank r takes queue entry qhead + r; pair data come from lane `slot`
                 const int r = lanes_below(idle);
                 const bool take = !act && r < qcount;
