@@ -279,9 +279,19 @@ __device__ __forceinline__ unsigned pack_ray(int slot, int i, int j) {
 // next round).  Lanes that did not win, or ran past their segment, point at private pad bins
 // and add 0, so the step body is branch-free.  Idle lanes are refilled from the ray queue.
 #ifndef NLOSGR_FSTEPS
-#define NLOSGR_FSTEPS 20
+#define NLOSGR_FSTEPS 28
 #endif
-constexpr int kSteps = NLOSGR_FSTEPS;     // bins per lane per drain round
+constexpr int kSteps = NLOSGR_FSTEPS;     // bins per lane per drain round (the largest; netf: kStepsNetf)
+#ifndef NLOSGR_FSTEPS_NETF
+#define NLOSGR_FSTEPS_NETF 20
+#endif
+constexpr int kStepsNetf = NLOSGR_FSTEPS_NETF;
+static_assert(kStepsNetf <= kSteps && kStepsNetf % 2 == 0, "the layouts' pads hold kSteps bins");
+// round 6: 28-bin rounds (with the refill deal at 56 idle lanes and 2 placement claim rounds) for the
+// no-occlusion and bin-integrated forwards: C3 734.8 -> 714.4 ms, C4 binint 1150 -> 1090 ms; netf measured
+// 883.7 -> 893.8 ms at 28 and keeps 20
+template <int MODE>
+__device__ __forceinline__ constexpr int fsteps() { return MODE == NLOSGR_MODE_NETF ? kStepsNetf : kSteps; }
 #ifndef NLOSGR_REFILL
 #define NLOSGR_REFILL 48
 #endif
@@ -525,7 +535,7 @@ constexpr int kFxTailBytes = 2048;           // workspace tail of the FX area: b
 #endif
 constexpr int kFxShift = NLOSGR_FXSHIFT;
 #ifndef NLOSGR_FXPLACE_ROUNDS
-#define NLOSGR_FXPLACE_ROUNDS 3
+#define NLOSGR_FXPLACE_ROUNDS 2
 #endif
 constexpr int kFxPlaceRounds = NLOSGR_FXPLACE_ROUNDS;   // claim rounds of the refill placement
 template <int CTRL>
@@ -713,7 +723,7 @@ __device__ __forceinline__ void tail_round(const Drain& d, const float t, float&
         const float cc = fast_exp2(2.f * d.ga);
         {
 #pragma unroll
-            for (int kv = 0; kv < kSteps / kVW; ++kv) {
+            for (int kv = 0; kv < fsteps<MODE>() / kVW; ++kv) {
                 const float v0 = (kv == 0 && o) ? 0.f : cur;
                 if (kv == 0) {
                     cur = o ? cur : cur * q;
@@ -749,7 +759,7 @@ __device__ __forceinline__ void tail_round(const Drain& d, const float t, float&
         const float pref = fast_exp2(d.al) * (0.88622692545275801f * frcp(d.beta));
         {
 #pragma unroll
-            for (int kv = 0; kv < kSteps / kVW; ++kv) {
+            for (int kv = 0; kv < fsteps<MODE>() / kVW; ++kv) {
                 float v[kVW];
 #pragma unroll
                 for (int jj = 0; jj < kVW; ++jj) {
@@ -791,7 +801,7 @@ __device__ __forceinline__ void tail_round(const Drain& d, const float t, float&
         auto gfac = [e1, e2, e3](float pv) { return fmaf(pv, fmaf(pv, e3, e2), e1); };
         {
 #pragma unroll
-            for (int kv = 0; kv < kSteps / kVW; ++kv) {
+            for (int kv = 0; kv < fsteps<MODE>() / kVW; ++kv) {
                 const float p0 = cur;
                 if (kv == 0) {
                     cur = o ? cur : cur * q;
@@ -812,7 +822,7 @@ __device__ __forceinline__ void tail_round(const Drain& d, const float t, float&
                 emit(kv, v0, v1);
             }
         }
-        T *= o ? kTfPow<kSteps - 1>() : kTfPow<kSteps>();   // T = T~ c0^(bins advanced)
+        T *= o ? kTfPow<fsteps<MODE>() - 1>() : kTfPow<fsteps<MODE>()>();   // T = T~ c0^(bins advanced)
     }
 }
 
@@ -1076,7 +1086,7 @@ __device__ __forceinline__ void fwd_body(const KArgs& k) {
                     const float cc = fast_exp2(2.f * d.ga);
                     float2* hb2 = reinterpret_cast<float2*>(hb);
 #pragma unroll
-                    for (int kv = 0; kv < kSteps / VW; ++kv) {
+                    for (int kv = 0; kv < fsteps<MODE>() / VW; ++kv) {
                         float v[VW];
 #pragma unroll
                         for (int jj = 0; jj < VW; ++jj) {
@@ -1098,7 +1108,7 @@ __device__ __forceinline__ void fwd_body(const KArgs& k) {
                         compiler_fence();
                     }
                 }
-                t += (float)(kSteps - o);
+                t += (float)(fsteps<MODE>() - o);
             } else {
             // netf, culled: pdf by the exp2 recurrence (kRecurrence), re-seeded per round
             constexpr bool REC = MODE == NLOSGR_MODE_NETF && !DENSE;
@@ -1110,7 +1120,7 @@ __device__ __forceinline__ void fwd_body(const KArgs& k) {
                 rcc = fast_exp2(2.f * d.ga);
             }
 #pragma unroll
-            for (int m = 0; m < kSteps; ++m) {
+            for (int m = 0; m < fsteps<MODE>(); ++m) {
                 const bool in = m < remw;
                 const float e2 = fmaf(d.ga, t * t, d.al);
                 float v;
@@ -1157,7 +1167,7 @@ __device__ __forceinline__ void fwd_body(const KArgs& k) {
             }
             }
             if (win) {
-                const int adv = QUAD ? kSteps - (d.pos & (VW - 1)) : kSteps;
+                const int adv = QUAD ? fsteps<MODE>() - (d.pos & (VW - 1)) : fsteps<MODE>();
                 d.t = t;
                 d.T = T;
                 d.xlo = xlo;
