@@ -939,7 +939,8 @@ __device__ __forceinline__ void fwd_body(const KArgs& k) {
             const int nidle = __popcll(idle);
             // the no-occlusion FX drain refills later: the deal's cost is per refill (REFILL 48 / 52 / 56 / 60 / 62:
             // 745.9 / 735.7 / 732.4 / 736.7 / 745.4 ms, same box)
-            constexpr int kRef = (FX && !BR && kFxPerm && MODE == NLOSGR_MODE_NOOCL) ? kRefillFx : kRefill;
+            constexpr int kRef = (FX && !BR && ((kFxPerm && MODE == NLOSGR_MODE_NOOCL) ||
+                                                (kFxPermNetf && MODE == NLOSGR_MODE_NETF))) ? kRefillFx : kRefill;
             if (qcount > 0 && (nidle >= kRef || !anymore)) {
                 // idle lane of rank r takes queue entry qhead + r; pair data come from lane `slot`
                 const int r = lanes_below(idle);
