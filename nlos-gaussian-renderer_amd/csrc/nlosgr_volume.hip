@@ -2593,12 +2593,18 @@ int sh_nsplit(const nlosgr_gaussians* g, const nlosgr_geometry* geo) {
 }
 // forward Gaussian splits per wall point: aim for 131072 workgroups (a 16k-workgroup grid of
 // one long workgroup per wall point leaves a ragged last round), at least 256 Gaussians per split
+#ifndef NLOSGR_FWD_SPLITS_MAX
+#define NLOSGR_FWD_SPLITS_MAX 8        // forward Gaussian splits per wall point, at most
+#endif
+#ifndef NLOSGR_FWD_WG_TARGET
+#define NLOSGR_FWD_WG_TARGET 131072    // forward workgroups aimed at (wall points x splits)
+#endif
 int fwd_nsplit(const nlosgr_gaussians* g, const nlosgr_geometry* geo) {
     if (geo->nwall <= 0) return 1;
-    int ns = (131072 + geo->nwall - 1) / geo->nwall;
+    int ns = (NLOSGR_FWD_WG_TARGET + geo->nwall - 1) / geo->nwall;
     const int byg = (g->ng + 255) / 256;
     if (ns > byg) ns = byg;
-    if (ns > 8) ns = 8;
+    if (ns > NLOSGR_FWD_SPLITS_MAX) ns = NLOSGR_FWD_SPLITS_MAX;
     return ns < 1 ? 1 : ns;
 }
 // forward partials: float [nfsplit][P][nr] (float drains) or, for the FX drain, u64 [P][nr]; then the FX
